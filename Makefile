@@ -1,0 +1,48 @@
+# Build of the MI355X classifier (gfx950) and of the CPU oracle.
+#   make            -> ingress-node-firewall_amd/lib/libinfw.so          (product: C ABI + HIP kernels)
+#                      ingress-node-firewall_amd/lib/libinfw_workload.so (bench/test workload generator)
+#                      oracle/build/liborc.so                            (test-only CPU oracle)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CC       ?= gcc
+PKG      := ingress-node-firewall_amd
+SRC      := $(PKG)/csrc
+OUT      := $(PKG)/lib
+OBJ      := $(PKG)/build
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
+EXTRA    ?=
+
+LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip
+LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
+HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
+
+all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so
+
+$(OBJ)/%.o: $(SRC)/% $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $@
+
+$(OUT)/libinfw.so: $(LIB_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIB_OBJS)
+
+$(OUT)/libinfw_workload.so: $(OBJ)/workload.hip.o
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $<
+
+oracle/build/liborc.so: oracle/infw_oracle.c oracle/infw_oracle.h
+	@mkdir -p oracle/build
+	$(CC) -O2 -g -fPIC -shared -pthread -Wall -Wextra -o $@ oracle/infw_oracle.c
+
+# kernel resource usage (VGPR/SGPR/LDS/occupancy) of the classify kernels
+resource-usage:
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $(SRC)/classify.hip -o /tmp/classify_ru.o
+
+asm:
+	@mkdir -p $(OBJ)/asm
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(OBJ)/asm/classify.s $(SRC)/classify.hip
+
+clean:
+	rm -rf $(OBJ) $(OUT) oracle/build
+
+.PHONY: all clean resource-usage asm

@@ -1,0 +1,266 @@
+/*
+ * infw.h — C ABI of the MI355X-native batched ingress-firewall classifier.
+ *
+ * This is the drop-in boundary for the hot path of pbmoses/ingress-node-firewall:
+ * the XDP program bpf/ingress_node_firewall_kernel.c and the map-population API
+ * of pkg/ebpf (cilium *ebpf.Map calls on ingress_node_firewall_table_map and
+ * ingress_node_firewall_statistics_map).  A cgo build of pkg/ebpf binds these
+ * symbols; every entry point below names the reference
+ * interface it replaces.
+ *
+ * Conventions (mirroring bpf(2), which is what the reference's Go code sees):
+ *   - return 0 on success or a negative errno (-EINVAL, -ENOENT, -EEXIST,
+ *     -ENOSPC, -ENOMEM, -ENODEV, -EIO);
+ *   - opaque handle, caller-owned buffers, no callbacks;
+ *   - control-plane calls (table_*, commit, stats_reset) are externally
+ *     serialised, like ebpfsyncer.go:62,72-73 (e.mu); infw_classify may run
+ *     concurrently on other threads/streams and each batch observes exactly
+ *     one committed table epoch.
+ *
+ * No torch types, no HIP types: device buffers and streams are plain pointers.
+ */
+#ifndef INFW_H
+#define INFW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Constants — bpf/ingress_node_firewall.h:4-23                              */
+/* ------------------------------------------------------------------------ */
+#define INFW_MAX_TARGETS 1024          /* ingress_node_firewall.h:13 (stats map size)   */
+#define INFW_MAX_RULES_PER_TARGET 100  /* ingress_node_firewall.h:14                    */
+#define INFW_MAX_EVENT_DATA 256        /* ingress_node_firewall.h:15                    */
+#define INFW_INVALID_RULE_ID 0         /* ingress_node_firewall.h:16                    */
+#define INFW_XDP_ABORTED 0             /* UNDEF, ingress_node_firewall.h:10             */
+#define INFW_XDP_DROP 1                /* DENY,  ingress_node_firewall.h:11             */
+#define INFW_XDP_PASS 2                /* ALLOW, ingress_node_firewall.h:12             */
+#define INFW_MAX_PREFIXLEN 160         /* 8 * sizeof(ifindex + ip_data): LPM data bits   */
+
+/* BPF map update flags (uapi/linux/bpf.h), accepted by infw_table_update.   */
+#define INFW_BPF_ANY 0
+#define INFW_BPF_NOEXIST 1
+#define INFW_BPF_EXIST 2
+
+/* Result word: ingress_node_firewall.h:18-23 (SET_ACTIONRULE_RESPONSE).     */
+#define INFW_RESULT(action, rule_id) \
+    ((uint32_t)((((uint32_t)(rule_id)) & 0xFFFFFFu) << 8 | ((action) & 0xFFu)))
+#define INFW_GET_ACTION(r) ((uint8_t)((r) & 0xFFu))
+#define INFW_GET_RULE_ID(r) ((uint16_t)(((r) >> 8) & 0xFFFFFFu))
+
+/* ------------------------------------------------------------------------ */
+/* Struct ABI — byte-identical to bpf/ingress_node_firewall.h:45-91 and to   */
+/* the bpf2go mirrors pkg/ebpf/bpf_bpfel.go:16-51 as marshalled by           */
+/* cilium/ebpf sysenc (packed, little-endian).  Skipped if the reference     */
+/* header was included first.                                                */
+/* ------------------------------------------------------------------------ */
+#ifndef __INGRESS_NODE_FIREWALL__
+struct ruleStatistics_st {            /* ingress_node_firewall.h:45-54, 32 B */
+    struct allow_stats_st {
+        uint64_t packets;
+        uint64_t bytes;
+    } allow_stats;
+    struct deny_stats_st {
+        uint64_t packets;
+        uint64_t bytes;
+    } deny_stats;
+};
+
+struct event_hdr_st {                 /* ingress_node_firewall.h:58-64, 8 B  */
+    uint16_t ifId;
+    uint16_t ruleId;
+    uint8_t action;
+    uint8_t pad;
+    uint16_t pktLength;
+} __attribute__((packed));
+
+struct ruleType_st {                  /* ingress_node_firewall.h:69-77, 12 B */
+    uint32_t ruleId;
+    uint8_t protocol;
+    uint16_t dstPortStart;
+    uint16_t dstPortEnd;
+    uint8_t icmpType;
+    uint8_t icmpCode;
+    uint8_t action;
+} __attribute__((packed));
+
+struct lpm_ip_key_st {                /* ingress_node_firewall.h:83-87, 24 B */
+    uint32_t prefixLen;
+    uint32_t ingress_ifindex;
+    uint8_t ip_data[16];
+} __attribute__((packed));
+
+struct rulesVal_st {                  /* ingress_node_firewall.h:89-91, 1200 B */
+    struct ruleType_st rules[INFW_MAX_RULES_PER_TARGET];
+} __attribute__((packed));
+#endif /* __INGRESS_NODE_FIREWALL__ */
+
+/* ------------------------------------------------------------------------ */
+/* Packet batch: struct-of-arrays header tuples, 32 B per packet.            */
+/* One tuple carries exactly the frame bytes kernel.c reads                  */
+/* (ingress_node_firewall_main :412-457, ip_extract_l4info :95-174):         */
+/*   saddr   16 B  frame[26..29] (IPv4, bytes 4..15 ignored) or frame[22..37] */
+/*   ifindex  4 B  xdp_md.ingress_ifindex                                     */
+/*   pkt_len  4 B  bpf_xdp_get_buff_len(ctx) (stats byte count)               */
+/*   meta     4 B  bits 0..15 ethertype (frame[12]<<8|frame[13]),             */
+/*                 bits 16..23 L3 next-proto (frame[23] v4 / frame[20] v6),   */
+/*                 bits 24..31 min(linear length, 255) (truncation checks)    */
+/*   l4word   4 B  frame[L4..L4+3] little-endian, L4 = 34 (v4) / 54 (v6),     */
+/*                 bytes past the linear length read as 0                     */
+/* All pointers are device pointers on the device the batch is classified on. */
+/* saddr must be 16-byte aligned.                                             */
+/* ------------------------------------------------------------------------ */
+struct infw_batch_soa {
+    const uint8_t *saddr;
+    const uint32_t *ifindex;
+    const uint32_t *pkt_len;
+    const uint32_t *meta;
+    const uint32_t *l4word;
+};
+
+#define INFW_META(ethertype, proto, caplen)                                    \
+    ((uint32_t)((ethertype) & 0xFFFFu) | ((uint32_t)((proto) & 0xFFu) << 16) | \
+     ((uint32_t)((caplen) > 255u ? 255u : (caplen)) << 24))
+
+typedef struct infw_ctx infw_ctx;
+
+/* ------------------------------------------------------------------------ */
+/* Lifecycle — replaces NewIngNodeFwController (loader.go:56-112) and Close */
+/* (loader.go:306-333) for the table + statistics maps.                      */
+/* ------------------------------------------------------------------------ */
+/* hip_devices: HIP device ordinals the context replicates its tables onto;   */
+/* NULL/n_dev=0 means {current device}.  max_entries: LPM capacity (the       */
+/* reference's MAX_TARGETS=1024 at kernel.c:54; 0 selects 1<<22).            */
+/* Without INFW_F_HOST_ONLY, -ENODEV when no HIP device is visible: there is   */
+/* no CPU classification path.                                                */
+#define INFW_F_HOST_ONLY 0x1u   /* control plane only: map API + compile, no    */
+                                /* device tables; infw_classify -> -ENODEV     */
+#define INFW_F_KEEP_HOST_IMAGE 0x2u /* keep the compiled host table image for  */
+                                    /* infw_debug_walk (tests)                 */
+int infw_create(infw_ctx **out, const int *hip_devices, int n_dev,
+                uint32_t max_entries, uint32_t flags);
+void infw_destroy(infw_ctx *ctx);
+int infw_num_devices(const infw_ctx *ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Table map — ingress_node_firewall_table_map (kernel.c:50-57, LPM_TRIE     */
+/* key 24 B / value 1200 B).  Calls edit the PENDING set with the kernel's   */
+/* LPM-trie map semantics; infw_table_commit publishes it to the GPUs.       */
+/* ------------------------------------------------------------------------ */
+/* Map.Update(key, val, flags)   loader.go:203  (addOrUpdateRules)           */
+/*   -EINVAL prefixLen>160, prefixLen<32 (never produced by BuildEBPFKey,    */
+/*           loader.go:543; the GPU tables key on the exact ifindex),         */
+/*           flags>BPF_EXIST;  -EEXIST / -ENOENT per NOEXIST / EXIST;         */
+/*   -ENOSPC when a new key would exceed max_entries.                        */
+int infw_table_update(infw_ctx *ctx, const struct lpm_ip_key_st *key,
+                      const struct rulesVal_st *val, uint64_t flags);
+/* Batch form (BPF_MAP_UPDATE_BATCH): val_index==NULL -> keys[i]:vals[i],     */
+/* else keys[i]:vals[val_index[i]].  Stops at the first error; *done (may be  */
+/* NULL) receives the number of keys applied.                                 */
+int infw_table_update_batch(infw_ctx *ctx, const struct lpm_ip_key_st *keys,
+                            const struct rulesVal_st *vals, const uint32_t *val_index,
+                            uint64_t n, uint64_t flags, uint64_t *done);
+/* Map.Delete(key)               loader.go:640  (purgeKeys): exact prefix.    */
+int infw_table_delete(infw_ctx *ctx, const struct lpm_ip_key_st *key);
+/* Map.Iterate() key walk        loader.go:293,558 (getStaleKeys,            */
+/* GetBPFMapContentForTest): key==NULL or absent -> first key; -ENOENT at end. */
+/* Order is the LPM trie's post-order (children before parents, 0-bit first). */
+int infw_table_get_next_key(infw_ctx *ctx, const struct lpm_ip_key_st *key,
+                            struct lpm_ip_key_st *next);
+/* Map.Lookup(key, &val): longest-prefix match over entries with              */
+/* prefixLen <= key->prefixLen (BPF LPM trie lookup semantics).               */
+int infw_table_lookup(infw_ctx *ctx, const struct lpm_ip_key_st *key,
+                      struct rulesVal_st *val);
+int infw_table_count(infw_ctx *ctx, uint64_t *n_entries);
+/* End of IngressNodeFwRulesLoader (loader.go:189-193): compile the pending   */
+/* set into GPU tables and swap epochs; in-flight batches finish on the old.  */
+int infw_table_commit(infw_ctx *ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Data path — replaces the per-frame XDP entry ingress_node_firewall_process */
+/* (kernel.c:459-462) with one batched launch.                                */
+/*   result_words[i] = the `result` of ingress_node_firewall_main (:418-442): */
+/*                     (ruleId & 0xFFFFFF) << 8 | action, 0 = UNDEF;          */
+/*   xdp_verdicts[i] = XDP return code (1 DROP / 2 PASS);                     */
+/*   statistics      = per-rule allow/deny packets+bytes added on the device  */
+/*                     (kernel.c:361-390), one slot per device.               */
+/* Either output may be NULL.  stream: hipStream_t (NULL = default stream).   */
+/* The call is asynchronous with respect to the host.                         */
+/* ------------------------------------------------------------------------ */
+int infw_classify(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
+                  uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Statistics — ingress_node_firewall_statistics_map (kernel.c:36-41,        */
+/* PERCPU_ARRAY[1024] of ruleStatistics_st).  One slot per device plays the  */
+/* role of one per-CPU slot; readers sum slots like statistics.go:126-157.   */
+/* ------------------------------------------------------------------------ */
+/* Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt)  statistics.go:127       */
+/* per_slot must hold infw_num_devices() entries; -ENOENT for rule >= 1024.   */
+int infw_stats_read(infw_ctx *ctx, uint32_t rule_id, struct ruleStatistics_st *per_slot,
+                    int *n_slots);
+/* All 1024 rules summed over slots (u64 wrap-around like the kernel).        */
+int infw_stats_read_all(infw_ctx *ctx, struct ruleStatistics_st out[INFW_MAX_TARGETS]);
+int infw_stats_reset(infw_ctx *ctx);
+/* Redirect device `dev`'s statistics slot to caller-owned device memory of   */
+/* 1024*32 B (e.g. a tensor that an RCCL all-reduce then sums across GPUs).   */
+/* NULL restores the context-owned slot.  Contents are not copied.            */
+int infw_stats_bind(infw_ctx *ctx, int dev, uint64_t *device_stats);
+/* Device pointer of device `dev`'s current statistics slot.                  */
+int infw_stats_device_ptr(infw_ctx *ctx, int dev, uint64_t **device_stats);
+
+/* ------------------------------------------------------------------------ */
+/* Control-plane encoders — the Go helpers whose byte output is the contract */
+/* of the table map.  Pure host functions (no device needed).                */
+/* ------------------------------------------------------------------------ */
+/* BuildEBPFKey(ifID, cidr)  loader.go:530-547.  -EINVAL on a bad CIDR.      */
+int infw_build_ebpf_key(uint32_t if_id, const char *cidr, struct lpm_ip_key_st *key);
+/* One IngressNodeFirewallProtocolRule -> rulesVal_st slot [order]            */
+/* (makeIngressFwRulesMap loader.go:435-515, utils.go:13-60).                 */
+/*   protocol: "TCP","UDP","SCTP","ICMP","ICMPv6" or "" (no protocolConfig)   */
+/*   ports:    "N" or "A-B" (TCP/UDP/SCTP), NULL/"" otherwise                 */
+/*   action:   "Allow" or "Deny"                                              */
+/* -EINVAL for the cases the Go code rejects; -E2BIG for order >= 100 (the Go */
+/* code panics on an out-of-range array index there, loader.go:437).          */
+int infw_make_rule(struct rulesVal_st *val, uint32_t order, const char *protocol,
+                   const char *ports, uint8_t icmp_type, uint8_t icmp_code,
+                   const char *action);
+
+/* ------------------------------------------------------------------------ */
+/* Introspection for tests and the bench.                                     */
+/* ------------------------------------------------------------------------ */
+struct infw_table_info {
+    uint64_t epoch;            /* number of successful commits                */
+    uint64_t n_entries;        /* committed LPM entries                       */
+    uint32_t n_if_slots;       /* distinct ingress ifindexes                  */
+    uint32_t n_lists;          /* interned rule lists                         */
+    uint64_t n_rules;          /* GPU rule records over all lists/classes     */
+    uint64_t n_tbl8_groups;    /* DIR-24-8 second-level groups                */
+    uint32_t n_long_levels;    /* distinct IPv6 prefix lengths > /32          */
+    uint64_t n_long_entries;   /* long-prefix hash entries incl. markers      */
+    uint64_t device_bytes;     /* table bytes resident per device             */
+    double compile_ms;         /* host compile time of the last commit        */
+    double upload_ms;          /* H2D time of the last commit                 */
+};
+int infw_table_info(infw_ctx *ctx, struct infw_table_info *info);
+/* Verification hook for tests/ only — never called by infw_classify: walks     */
+/* the last committed HOST table image (INFW_F_HOST_ONLY or                      */
+/* INFW_F_KEEP_HOST_IMAGE contexts) with the same lookup code the kernel runs,   */
+/* so the table compiler can be checked against the oracle on a CPU-only box.   */
+/* tuples: n x 8 u32 {saddr[4], ifindex, pkt_len, meta, l4word}.                */
+/* out: result words (same meaning as infw_classify's).  -ENODATA w/o image.    */
+int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t *out);
+/* Last error string of this thread (static storage).                          */
+const char *infw_last_error(void);
+/* ABI version (bumped on incompatible change).                                */
+#define INFW_ABI_VERSION 1
+int infw_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INFW_H */

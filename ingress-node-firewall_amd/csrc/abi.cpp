@@ -1,0 +1,394 @@
+// abi.cpp — libinfw C ABI (include/infw.h): context, pending table map,
+// epoch commit + upload, classify dispatch, statistics slots.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <memory>
+#include <mutex>
+
+#include "infw_internal.h"
+
+extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
+                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats,
+                                    uint32_t grid, hipStream_t stream);
+
+namespace infw {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+#define HIP_OK(expr)                                                             \
+    do {                                                                         \
+        hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess) {                                                  \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));       \
+            return -EIO;                                                         \
+        }                                                                        \
+    } while (0)
+
+// Restores the caller's current HIP device (callers such as torch keep their own).
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// One epoch's tables resident on one device.
+struct DeviceEpoch {
+    int ordinal = -1;
+    std::vector<void *> allocs;
+    infw_dev_tables view;
+    uint64_t bytes = 0;
+    ~DeviceEpoch() {
+        if (ordinal < 0) return;
+        DeviceGuard g(ordinal);
+        (void)hipDeviceSynchronize();  // batches launched on this epoch have finished
+        for (void *p : allocs) (void)hipFree(p);
+    }
+};
+
+struct Device {
+    int ordinal = 0;
+    uint32_t grid = 2048;
+    uint64_t *stats_own = nullptr;
+    uint64_t *stats = nullptr;
+    std::shared_ptr<DeviceEpoch> epoch;
+};
+
+}  // namespace infw
+
+using namespace infw;
+
+struct infw_ctx {
+    std::vector<Device> devs;
+    uint32_t flags = 0;
+    PendingMap map;
+    std::unique_ptr<HostTables> host_image;  // INFW_F_HOST_ONLY / INFW_F_KEEP_HOST_IMAGE
+    std::mutex epoch_mu;  // guards devs[*].epoch swaps vs classify snapshots
+    uint64_t epoch_no = 0;
+    uint64_t committed_gen = ~0ull;
+    struct infw_table_info info{};
+};
+
+template <class T>
+static int upload(DeviceEpoch &ep, const std::vector<T> &v, const T **dst) {
+    void *p = nullptr;
+    size_t bytes = v.size() * sizeof(T);
+    if (bytes == 0) bytes = sizeof(T);
+    HIP_OK(hipMalloc(&p, bytes));
+    ep.allocs.push_back(p);
+    if (!v.empty()) HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    ep.bytes += bytes;
+    *dst = static_cast<const T *>(p);
+    return 0;
+}
+
+static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {
+    DeviceGuard g(ordinal);
+    if (!g.ok) {
+        set_error("hipSetDevice failed");
+        return -ENODEV;
+    }
+    auto ep = std::make_shared<DeviceEpoch>();
+    ep->ordinal = ordinal;
+    infw_dev_tables &t = ep->view;
+    memset(&t, 0, sizeof(t));
+    int rc = 0;
+    if ((rc = upload(*ep, h.if_keys, &t.if_keys)) || (rc = upload(*ep, h.if_slot, &t.if_slot)) ||
+        (rc = upload(*ep, h.tbl24, &t.tbl24)) || (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
+        (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
+        (rc = upload(*ep, h.rules, &t.rules)))
+        return rc;
+    t.if_mask = (uint32_t)h.if_keys.size() - 1;
+    t.n_slots = h.n_slots;
+    t.lmask = h.ltab.size() - 1;
+    t.n_levels = (uint32_t)h.levels.size();
+    for (size_t i = 0; i < h.levels.size(); i++) t.levels[i] = h.levels[i];
+    out = ep;
+    return 0;
+}
+
+extern "C" {
+
+const char *infw_last_error(void) { return g_err.c_str(); }
+int infw_abi_version(void) { return INFW_ABI_VERSION; }
+
+int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_entries,
+                uint32_t flags) {
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    std::unique_ptr<infw_ctx> ctx(new infw_ctx());
+    ctx->flags = flags;
+    ctx->map.max_entries = max_entries ? max_entries : (1u << 22);
+    if (flags & INFW_F_HOST_ONLY) {
+        int rc = infw_table_commit(ctx.get());
+        if (rc) return rc;
+        ctx->epoch_no = 0;
+        ctx->info.epoch = 0;
+        *out = ctx.release();
+        return 0;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("no HIP device visible: the classifier has no CPU fallback");
+        return -ENODEV;
+    }
+    std::vector<int> ords;
+    if (!hip_devices || n_dev <= 0) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+        ords.push_back(cur);
+    } else {
+        for (int i = 0; i < n_dev; i++) {
+            if (hip_devices[i] < 0 || hip_devices[i] >= count) {
+                set_error("device ordinal out of range");
+                return -ENODEV;
+            }
+            ords.push_back(hip_devices[i]);
+        }
+    }
+    for (int o : ords) {
+        Device d;
+        d.ordinal = o;
+        DeviceGuard g(o);
+        if (!g.ok) {
+            set_error("hipSetDevice failed");
+            return -ENODEV;
+        }
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o);
+        d.grid = (uint32_t)cus * 6;  // 24 KiB LDS/workgroup -> 6 resident per CU
+        HIP_OK(hipMalloc(&d.stats_own, INFW_MAX_TARGETS * sizeof(ruleStatistics_st)));
+        HIP_OK(hipMemset(d.stats_own, 0, INFW_MAX_TARGETS * sizeof(ruleStatistics_st)));
+        d.stats = d.stats_own;
+        ctx->devs.push_back(d);
+    }
+    // an empty epoch so classify works before the first commit (everything misses)
+    int rc = infw_table_commit(ctx.get());
+    if (rc) return rc;
+    ctx->epoch_no = 0;
+    ctx->info.epoch = 0;
+    *out = ctx.release();
+    return 0;
+}
+
+void infw_destroy(infw_ctx *ctx) {
+    if (!ctx) return;
+    for (auto &d : ctx->devs) {
+        d.epoch.reset();
+        DeviceGuard g(d.ordinal);
+        (void)hipDeviceSynchronize();
+        if (d.stats_own) (void)hipFree(d.stats_own);
+    }
+    delete ctx;
+}
+
+int infw_num_devices(const infw_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int infw_table_update(infw_ctx *ctx, const lpm_ip_key_st *key, const rulesVal_st *val,
+                      uint64_t flags) {
+    if (!ctx || !key || !val) return -EINVAL;
+    return ctx->map.update(key, reinterpret_cast<const uint8_t *>(val), flags);
+}
+
+int infw_table_update_batch(infw_ctx *ctx, const lpm_ip_key_st *keys, const rulesVal_st *vals,
+                            const uint32_t *val_index, uint64_t n, uint64_t flags, uint64_t *done) {
+    if (done) *done = 0;
+    if (!ctx || (n && (!keys || !vals))) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        const rulesVal_st *v = val_index ? &vals[val_index[i]] : &vals[i];
+        int rc = ctx->map.update(&keys[i], reinterpret_cast<const uint8_t *>(v), flags);
+        if (rc) return rc;
+        if (done) *done = i + 1;
+    }
+    return 0;
+}
+
+int infw_table_delete(infw_ctx *ctx, const lpm_ip_key_st *key) {
+    if (!ctx || !key) return -EINVAL;
+    return ctx->map.remove(key);
+}
+
+int infw_table_get_next_key(infw_ctx *ctx, const lpm_ip_key_st *key, lpm_ip_key_st *next) {
+    if (!ctx || !next) return -EINVAL;
+    return ctx->map.next_key(key, next);
+}
+
+int infw_table_lookup(infw_ctx *ctx, const lpm_ip_key_st *key, rulesVal_st *val) {
+    if (!ctx || !key) return -EINVAL;
+    return ctx->map.lookup(key, reinterpret_cast<uint8_t *>(val));
+}
+
+int infw_table_count(infw_ctx *ctx, uint64_t *n) {
+    if (!ctx || !n) return -EINVAL;
+    *n = ctx->map.nodes.size();
+    return 0;
+}
+
+int infw_table_commit(infw_ctx *ctx) {
+    if (!ctx) return -EINVAL;
+    auto t0 = std::chrono::steady_clock::now();
+    HostTables h;
+    int rc = compile_tables(ctx->map, h);
+    if (rc) return rc;
+    auto t1 = std::chrono::steady_clock::now();
+    std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size());
+    for (size_t i = 0; i < ctx->devs.size(); i++) {
+        rc = upload_epoch(h, ctx->devs[i].ordinal, eps[i]);
+        if (rc) return rc;  // nothing swapped: the previous epoch stays live
+    }
+    auto t2 = std::chrono::steady_clock::now();
+    std::vector<std::shared_ptr<DeviceEpoch>> old(ctx->devs.size());
+    {
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        for (size_t i = 0; i < ctx->devs.size(); i++) {
+            old[i] = ctx->devs[i].epoch;
+            ctx->devs[i].epoch = eps[i];
+        }
+        ctx->epoch_no++;
+    }
+    old.clear();  // waits for batches still running on the old tables, then frees them
+    struct infw_table_info &in = ctx->info;
+    in.epoch = ctx->epoch_no;
+    in.n_entries = h.n_entries;
+    in.n_if_slots = h.n_slots;
+    in.n_lists = h.n_lists;
+    in.n_rules = h.rules.size();
+    in.n_tbl8_groups = h.tbl8.size() / 256;
+    in.n_long_levels = (uint32_t)h.levels.size();
+    in.n_long_entries = h.n_long_entries;
+    in.device_bytes = eps.empty() ? 0 : eps[0]->bytes;
+    in.compile_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    ctx->committed_gen = ctx->map.generation;
+    if (ctx->flags & (INFW_F_HOST_ONLY | INFW_F_KEEP_HOST_IMAGE))
+        ctx->host_image.reset(new HostTables(std::move(h)));
+    return 0;
+}
+
+int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t *out) {
+    if (!ctx || (n && (!tuples || !out))) return -EINVAL;
+    if (!ctx->host_image) {
+        set_error("debug_walk: no host table image (create with INFW_F_HOST_ONLY or INFW_F_KEEP_HOST_IMAGE)");
+        return -ENODATA;
+    }
+    const infw_dev_tables t = ctx->host_image->view();
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t *q = tuples + 8 * i;
+        int cls = 0;
+        uint32_t val = 0, result = 0;
+        int pk = infw_parse(q[6], q[7], &cls, &val);
+        if (pk >= INFW_PK_V4) {
+            uint32_t l1 = infw_lpm(t, pk, q[4], q);
+            if (l1) result = infw_scan_serial(t, t.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls], val);
+        }
+        out[i] = result;
+    }
+    return 0;
+}
+
+int infw_table_info(infw_ctx *ctx, struct infw_table_info *info) {
+    if (!ctx || !info) return -EINVAL;
+    *info = ctx->info;
+    return 0;
+}
+
+int infw_classify(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n,
+                  uint32_t *result_words, uint8_t *xdp_verdicts, void *stream) {
+    if (!ctx || !in) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("classify: host-only context has no device tables");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (n && (!in->saddr || !in->ifindex || !in->pkt_len || !in->meta || !in->l4word)) {
+        set_error("classify: null input stream");
+        return -EINVAL;
+    }
+    if (((uintptr_t)in->saddr & 15) != 0) {
+        set_error("classify: saddr must be 16-byte aligned");
+        return -EINVAL;
+    }
+    Device &d = ctx->devs[dev];
+    std::shared_ptr<DeviceEpoch> ep;
+    {
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        ep = d.epoch;
+    }
+    DeviceGuard g(d.ordinal);
+    if (!g.ok) {
+        set_error("hipSetDevice failed");
+        return -ENODEV;
+    }
+    int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.grid,
+                                  static_cast<hipStream_t>(stream));
+    if (rc) {
+        set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    return 0;
+}
+
+int infw_stats_read(infw_ctx *ctx, uint32_t rule_id, ruleStatistics_st *per_slot, int *n_slots) {
+    if (!ctx || !per_slot) return -EINVAL;
+    if (rule_id >= INFW_MAX_TARGETS) return -ENOENT;
+    for (size_t i = 0; i < ctx->devs.size(); i++) {
+        DeviceGuard g(ctx->devs[i].ordinal);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(&per_slot[i], ctx->devs[i].stats + 4 * rule_id, sizeof(ruleStatistics_st),
+                         hipMemcpyDeviceToHost));
+    }
+    if (n_slots) *n_slots = (int)ctx->devs.size();
+    return 0;
+}
+
+int infw_stats_read_all(infw_ctx *ctx, ruleStatistics_st out[INFW_MAX_TARGETS]) {
+    if (!ctx || !out) return -EINVAL;
+    memset(out, 0, sizeof(ruleStatistics_st) * INFW_MAX_TARGETS);
+    std::vector<ruleStatistics_st> tmp(INFW_MAX_TARGETS);
+    for (auto &d : ctx->devs) {
+        DeviceGuard g(d.ordinal);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(tmp.data(), d.stats, sizeof(ruleStatistics_st) * INFW_MAX_TARGETS,
+                         hipMemcpyDeviceToHost));
+        for (int k = 0; k < INFW_MAX_TARGETS; k++) {
+            out[k].allow_stats.packets += tmp[k].allow_stats.packets;
+            out[k].allow_stats.bytes += tmp[k].allow_stats.bytes;
+            out[k].deny_stats.packets += tmp[k].deny_stats.packets;
+            out[k].deny_stats.bytes += tmp[k].deny_stats.bytes;
+        }
+    }
+    return 0;
+}
+
+int infw_stats_reset(infw_ctx *ctx) {
+    if (!ctx) return -EINVAL;
+    for (auto &d : ctx->devs) {
+        DeviceGuard g(d.ordinal);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemset(d.stats, 0, sizeof(ruleStatistics_st) * INFW_MAX_TARGETS));
+    }
+    return 0;
+}
+
+int infw_stats_bind(infw_ctx *ctx, int dev, uint64_t *device_stats) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (((uintptr_t)device_stats & 7) != 0) return -EINVAL;
+    ctx->devs[dev].stats = device_stats ? device_stats : ctx->devs[dev].stats_own;
+    return 0;
+}
+
+int infw_stats_device_ptr(infw_ctx *ctx, int dev, uint64_t **device_stats) {
+    if (!ctx || !device_stats || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    *device_stats = ctx->devs[dev].stats;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// infw_internal.h — host-side types of libinfw (not part of the C ABI).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <array>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/infw.h"
+#include "infw_tables.h"
+
+namespace infw {
+
+void set_error(const std::string &msg);
+
+// ------------------------------------------------------------------------
+// Pending LPM map with the kernel LPM-trie semantics (kernel.c:50-57 map,
+// kernel/bpf/lpm_trie.c).  A node is identified by (prefixLen, data masked
+// to prefixLen); the stored data keeps the last writer's host bits, which
+// get_next_key returns (trie_get_next_key copies node->data).
+// ------------------------------------------------------------------------
+struct NodeKey {
+    uint32_t plen;
+    uint8_t md[20];  // [ifindex LE][ip_data], masked to plen bits
+    bool operator==(const NodeKey &o) const { return plen == o.plen && memcmp(md, o.md, 20) == 0; }
+};
+struct NodeKeyHash {
+    size_t operator()(const NodeKey &k) const;
+};
+// Trie post-order: descendants before ancestors, 0-branch before 1-branch.
+struct PostOrderLess {
+    bool operator()(const NodeKey &a, const NodeKey &b) const;
+};
+struct NodeVal {
+    uint8_t data[20];
+    uint32_t vid;  // interned value id
+};
+
+struct ValuePool {
+    std::vector<std::array<uint8_t, 1200>> vals;
+    std::unordered_multimap<uint64_t, uint32_t> index;
+    uint32_t intern(const uint8_t *v);
+};
+
+struct PendingMap {
+    uint32_t max_entries = 0;
+    std::unordered_map<NodeKey, NodeVal, NodeKeyHash> nodes;
+    std::set<NodeKey, PostOrderLess> order;
+    uint64_t len_count[INFW_MAX_PREFIXLEN + 1] = {};
+    ValuePool pool;
+    uint64_t generation = 0;  // bumped on every successful edit
+
+    int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
+    int remove(const lpm_ip_key_st *key);
+    int lookup(const lpm_ip_key_st *key, uint8_t *val) const;
+    int next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const;
+};
+
+void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes);
+
+// ------------------------------------------------------------------------
+// One compiled epoch on the host (tables.cpp).
+// ------------------------------------------------------------------------
+struct HostTables {
+    std::vector<uint32_t> if_keys, if_slot;
+    uint32_t n_slots = 0;
+    std::vector<uint32_t> tbl24;  // n_slots << 24
+    std::vector<uint32_t> tbl8;
+    std::vector<infw_long_entry> ltab;
+    std::vector<uint8_t> levels;
+    std::vector<uint64_t> desc;
+    std::vector<uint64_t> rules;
+    uint32_t n_lists = 0;
+    uint64_t n_entries = 0;
+    uint64_t n_long_entries = 0;
+    // A host view with the same walk functions as the device (self-test only).
+    infw_dev_tables view() const;
+};
+
+int compile_tables(const PendingMap &m, HostTables &out);
+
+// Class-filtered GPU rule records of one 1200-B value (appended to rules).
+void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE]);
+
+}  // namespace infw

@@ -1,0 +1,479 @@
+// tables.cpp — the pending LPM map (control-plane semantics of
+// ingress_node_firewall_table_map) and its compilation into the GPU table
+// layout described in infw_tables.h.
+#include <errno.h>
+
+#include <algorithm>
+#include <numeric>
+
+#include "infw_internal.h"
+
+namespace infw {
+
+static inline uint32_t rd_le32(const uint8_t *p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+static uint64_t fnv64(const uint8_t *p, size_t n, uint64_t h) {
+    for (size_t i = 0; i < n; i++) {
+        h ^= p[i];
+        h *= 0x100000001B3ull;
+    }
+    h ^= h >> 31;
+    h *= 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 29);
+}
+
+size_t NodeKeyHash::operator()(const NodeKey &k) const {
+    return (size_t)fnv64(k.md, 20, 0xCBF29CE484222325ull ^ ((uint64_t)k.plen << 40));
+}
+
+static inline int bit_at(const uint8_t *d, uint32_t i) { return (d[i >> 3] >> (7 - (i & 7))) & 1; }
+
+bool PostOrderLess::operator()(const NodeKey &a, const NodeKey &b) const {
+    uint32_t mn = a.plen < b.plen ? a.plen : b.plen;
+    // first differing bit within the common length decides (0-branch first)
+    uint32_t full = mn >> 3;
+    for (uint32_t i = 0; i < full; i++) {
+        if (a.md[i] != b.md[i]) {
+            uint8_t x = a.md[i] ^ b.md[i];
+            int msb = 7;
+            while (!((x >> msb) & 1)) msb--;
+            return ((a.md[i] >> msb) & 1) < ((b.md[i] >> msb) & 1);
+        }
+    }
+    for (uint32_t i = full * 8; i < mn; i++) {
+        int x = bit_at(a.md, i), y = bit_at(b.md, i);
+        if (x != y) return x < y;
+    }
+    return a.plen > b.plen;  // descendant (longer) before ancestor; equal -> false
+}
+
+void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes) {
+    for (int i = 0; i < nbytes; i++) {
+        uint32_t b0 = 8u * (uint32_t)i;
+        if (plen >= b0 + 8) out[i] = in[i];
+        else if (plen <= b0) out[i] = 0;
+        else out[i] = (uint8_t)(in[i] & (0xFFu << (8 - (plen - b0))));
+    }
+}
+
+uint32_t ValuePool::intern(const uint8_t *v) {
+    uint64_t h = fnv64(v, 1200, 0x84222325CBF29CE4ull);
+    auto range = index.equal_range(h);
+    for (auto it = range.first; it != range.second; ++it)
+        if (memcmp(vals[it->second].data(), v, 1200) == 0) return it->second;
+    uint32_t id = (uint32_t)vals.size();
+    vals.emplace_back();
+    memcpy(vals.back().data(), v, 1200);
+    index.emplace(h, id);
+    return id;
+}
+
+static NodeKey make_node(const lpm_ip_key_st *key) {
+    NodeKey k;
+    k.plen = key->prefixLen;
+    uint8_t data[20];
+    memcpy(data, &key->ingress_ifindex, 4);
+    memcpy(data + 4, key->ip_data, 16);
+    mask_bits(data, k.plen, k.md, 20);
+    return k;
+}
+
+// trie_update_elem (lpm_trie.c, Linux 6.18) order of checks.
+int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags) {
+    if (flags > INFW_BPF_EXIST) {
+        set_error("update: flags > BPF_EXIST");
+        return -EINVAL;
+    }
+    if (key->prefixLen > INFW_MAX_PREFIXLEN) {
+        set_error("update: prefixLen > 160");
+        return -EINVAL;
+    }
+    if (key->prefixLen < 32) {
+        // An entry shorter than the ifindex would match a set of interfaces;
+        // BuildEBPFKey never produces one (loader.go:543).
+        set_error("update: prefixLen < 32 (partial ifindex prefix) is not supported");
+        return -EINVAL;
+    }
+    NodeKey k = make_node(key);
+    auto it = nodes.find(k);
+    if (it != nodes.end()) {
+        if (flags == INFW_BPF_NOEXIST) return -EEXIST;
+        memcpy(it->second.data, &key->ingress_ifindex, 4);
+        memcpy(it->second.data + 4, key->ip_data, 16);
+        it->second.vid = pool.intern(val);
+        generation++;
+        return 0;
+    }
+    if (flags == INFW_BPF_EXIST) return -ENOENT;
+    if (nodes.size() >= max_entries) {
+        set_error("update: table map full");
+        return -ENOSPC;
+    }
+    NodeVal v;
+    memcpy(v.data, &key->ingress_ifindex, 4);
+    memcpy(v.data + 4, key->ip_data, 16);
+    v.vid = pool.intern(val);
+    nodes.emplace(k, v);
+    order.insert(k);
+    len_count[k.plen]++;
+    generation++;
+    return 0;
+}
+
+int PendingMap::remove(const lpm_ip_key_st *key) {
+    if (key->prefixLen > INFW_MAX_PREFIXLEN) return -EINVAL;
+    NodeKey k = make_node(key);
+    auto it = nodes.find(k);
+    if (it == nodes.end()) return -ENOENT;
+    nodes.erase(it);
+    order.erase(k);
+    len_count[k.plen]--;
+    generation++;
+    return 0;
+}
+
+int PendingMap::lookup(const lpm_ip_key_st *key, uint8_t *val) const {
+    uint32_t kp = key->prefixLen > INFW_MAX_PREFIXLEN ? INFW_MAX_PREFIXLEN : key->prefixLen;
+    uint8_t data[20];
+    memcpy(data, &key->ingress_ifindex, 4);
+    memcpy(data + 4, key->ip_data, 16);
+    for (int L = (int)kp; L >= 0; L--) {
+        if (!len_count[L]) continue;
+        NodeKey k;
+        k.plen = (uint32_t)L;
+        mask_bits(data, (uint32_t)L, k.md, 20);
+        auto it = nodes.find(k);
+        if (it != nodes.end()) {
+            if (val) memcpy(val, pool.vals[it->second.vid].data(), 1200);
+            return 0;
+        }
+    }
+    return -ENOENT;
+}
+
+int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
+    if (order.empty()) return -ENOENT;
+    auto it = order.begin();
+    if (key && key->prefixLen <= INFW_MAX_PREFIXLEN) {
+        NodeKey k = make_node(key);
+        if (nodes.count(k)) {
+            it = order.upper_bound(k);
+            if (it == order.end()) return -ENOENT;
+        }
+    }
+    const NodeVal &v = nodes.at(*it);
+    next->prefixLen = it->plen;
+    memcpy(&next->ingress_ifindex, v.data, 4);
+    memcpy(next->ip_data, v.data + 4, 16);
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// Rule lists.  For one 1200-B value, the rules each packet class can match,
+// in slot order (kernel.c:222-258 / :306-340), as {lo16, hi16, result32}:
+//   ruleId == 0                      skipped (:225-227)
+//   protocol 0                       every class, any value (:255-257)
+//   TCP/UDP/SCTP                     that class; end == 0 -> [start, start],
+//                                    else [start, end-1] (end-exclusive :241);
+//                                    an empty range never matches: dropped
+//   ICMP (1)                         IPv4 path only (:247): [type<<8|code]
+//   ICMPv6 (58)                      IPv6 path only (:329)
+//   any other protocol               can never match: dropped
+// result32 = SET_ACTIONRULE_RESPONSE(action, ruleId) (ingress_node_firewall.h:22).
+// ------------------------------------------------------------------------
+void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
+                       uint64_t desc_out[INFW_DESC_STRIDE]) {
+    std::vector<uint64_t> per[INFW_NCLS];
+    for (int i = 0; i < INFW_MAX_RULES_PER_TARGET; i++) {
+        const uint8_t *r = val + 12 * i;
+        uint32_t rule_id = rd_le32(r);
+        uint8_t proto = r[4];
+        uint16_t ps = (uint16_t)(r[5] | r[6] << 8), pe = (uint16_t)(r[7] | r[8] << 8);
+        uint8_t it = r[9], ic = r[10], action = r[11];
+        if (rule_id == INFW_INVALID_RULE_ID) continue;
+        uint64_t res = (uint64_t)INFW_RESULT(action, rule_id) << 32;
+        auto rec = [&](uint32_t lo, uint32_t hi) { return (uint64_t)lo | (uint64_t)hi << 16 | res; };
+        switch (proto) {
+        case 0:
+            for (int c = 0; c < INFW_NCLS; c++) per[c].push_back(rec(0, 0xFFFF));
+            break;
+        case 6:
+        case 17:
+        case 132: {
+            int c = proto == 6 ? INFW_CLS_TCP : proto == 17 ? INFW_CLS_UDP : INFW_CLS_SCTP;
+            if (pe == 0) per[c].push_back(rec(ps, ps));
+            else if (ps < pe) per[c].push_back(rec(ps, (uint32_t)pe - 1));
+            break;
+        }
+        case 1: {
+            uint32_t v = (uint32_t)it << 8 | ic;
+            per[INFW_CLS_ICMP4].push_back(rec(v, v));
+            break;
+        }
+        case 58: {
+            uint32_t v = (uint32_t)it << 8 | ic;
+            per[INFW_CLS_ICMP6].push_back(rec(v, v));
+            break;
+        }
+        default:
+            break;
+        }
+    }
+    for (int c = 0; c < INFW_DESC_STRIDE; c++) {
+        if (c >= INFW_NCLS || per[c].empty()) {
+            desc_out[c] = 0;
+            continue;
+        }
+        uint64_t off = rules.size();
+        rules.insert(rules.end(), per[c].begin(), per[c].end());
+        desc_out[c] = off | (uint64_t)per[c].size() << 32;
+    }
+}
+
+// ------------------------------------------------------------------------
+// Host open-addressed table for long-prefix nodes while compiling.
+// ------------------------------------------------------------------------
+namespace {
+struct LongNode {
+    uint64_t hi, lo;
+    uint32_t tag;
+    uint32_t real;  // list+1 of a real prefix at exactly this node, 0 = marker only
+};
+struct LongSet {
+    std::vector<LongNode> tab;
+    uint64_t mask = 0, n = 0;
+    void init(uint64_t expect) {
+        uint64_t cap = 1024;
+        while (cap < expect * 2) cap <<= 1;
+        tab.assign(cap, LongNode{0, 0, 0, 0});
+        mask = cap - 1;
+        n = 0;
+    }
+    LongNode *find_or_insert(uint32_t tag, uint64_t hi, uint64_t lo) {
+        uint64_t i = infw_long_hash(tag, hi, lo) & mask;
+        for (;;) {
+            LongNode &e = tab[i];
+            if (e.tag == 0) {
+                e.tag = tag; e.hi = hi; e.lo = lo; e.real = 0;
+                n++;
+                return &e;
+            }
+            if (e.tag == tag && e.hi == hi && e.lo == lo) return &e;
+            i = (i + 1) & mask;
+        }
+    }
+    const LongNode *find(uint32_t tag, uint64_t hi, uint64_t lo) const {
+        uint64_t i = infw_long_hash(tag, hi, lo) & mask;
+        for (;;) {
+            const LongNode &e = tab[i];
+            if (e.tag == 0) return nullptr;
+            if (e.tag == tag && e.hi == hi && e.lo == lo) return &e;
+            i = (i + 1) & mask;
+        }
+    }
+};
+struct ShortEnt {
+    uint32_t slot, a32, plen, list1;
+};
+}  // namespace
+
+int compile_tables(const PendingMap &m, HostTables &out) {
+    out = HostTables();
+    // --- slots: distinct ifindexes, ascending
+    std::vector<uint32_t> ifs;
+    ifs.reserve(64);
+    {
+        std::unordered_map<uint32_t, int> seen;
+        for (const auto &kv : m.nodes) {
+            uint32_t ifx = rd_le32(kv.first.md);
+            if (seen.emplace(ifx, 0).second) ifs.push_back(ifx);
+        }
+        std::sort(ifs.begin(), ifs.end());
+    }
+    out.n_slots = (uint32_t)ifs.size();
+    if (out.n_slots >= (1u << 23)) {
+        set_error("compile: too many ifindexes");
+        return -ENOSPC;
+    }
+    std::unordered_map<uint32_t, uint32_t> slot_of;
+    for (uint32_t s = 0; s < out.n_slots; s++) slot_of[ifs[s]] = s;
+    {
+        uint32_t cap = 16;
+        while (cap < 2 * out.n_slots) cap <<= 1;
+        out.if_keys.assign(cap, 0);
+        out.if_slot.assign(cap, INFW_IF_EMPTY);
+        for (uint32_t s = 0; s < out.n_slots; s++) {
+            uint32_t h = infw_if_hash(ifs[s]) & (cap - 1);
+            while (out.if_slot[h] != INFW_IF_EMPTY) h = (h + 1) & (cap - 1);
+            out.if_keys[h] = ifs[s];
+            out.if_slot[h] = s;
+        }
+    }
+
+    // --- rule lists: one per distinct referenced value
+    std::unordered_map<uint32_t, uint32_t> list_of_vid;
+    for (const auto &kv : m.nodes) {
+        uint32_t vid = kv.second.vid;
+        if (list_of_vid.count(vid)) continue;
+        uint32_t lid = (uint32_t)list_of_vid.size();
+        list_of_vid[vid] = lid;
+    }
+    out.n_lists = (uint32_t)list_of_vid.size();
+    out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
+    {
+        std::vector<std::pair<uint32_t, uint32_t>> by_lid(list_of_vid.begin(), list_of_vid.end());
+        std::sort(by_lid.begin(), by_lid.end(),
+                  [](const std::pair<uint32_t, uint32_t> &a, const std::pair<uint32_t, uint32_t> &b) {
+                      return a.second < b.second;
+                  });
+        for (auto &p : by_lid)
+            compile_rule_list(m.pool.vals[p.first].data(), out.rules, &out.desc[(size_t)p.second * INFW_DESC_STRIDE]);
+    }
+    if (out.rules.empty()) out.rules.push_back(0);
+
+    // --- split entries
+    std::vector<ShortEnt> shorts;
+    struct LongReal {
+        uint32_t slot, len, list1;
+        uint64_t hi, lo;
+    };
+    std::vector<LongReal> longs;
+    shorts.reserve(m.nodes.size());
+    for (const auto &kv : m.nodes) {
+        const NodeKey &k = kv.first;
+        uint32_t slot = slot_of[rd_le32(k.md)];
+        uint32_t P = k.plen - 32;
+        uint32_t list1 = list_of_vid[kv.second.vid] + 1;
+        const uint8_t *ip = k.md + 4;  // already masked to P bits
+        if (P <= 32) {
+            uint32_t a32 = (uint32_t)ip[0] << 24 | (uint32_t)ip[1] << 16 | (uint32_t)ip[2] << 8 | ip[3];
+            shorts.push_back(ShortEnt{slot, a32, P, list1});
+        } else {
+            uint64_t hi = 0, lo = 0;
+            for (int i = 0; i < 8; i++) hi = hi << 8 | ip[i];
+            for (int i = 8; i < 16; i++) lo = lo << 8 | ip[i];
+            longs.push_back(LongReal{slot, P, list1, hi, lo});
+        }
+    }
+    out.n_entries = m.nodes.size();
+
+    // --- DIR-24-8 over the unified 32-bit prefix space, per slot
+    if (out.n_slots) {
+        out.tbl24.assign((size_t)out.n_slots << 24, 0u);
+        std::sort(shorts.begin(), shorts.end(),
+                  [](const ShortEnt &a, const ShortEnt &b) { return a.plen < b.plen; });
+        for (const ShortEnt &e : shorts) {
+            uint32_t *t24 = &out.tbl24[(size_t)e.slot << 24];
+            if (e.plen <= 24) {
+                uint32_t start = e.a32 >> 8;
+                uint32_t cnt = 1u << (24 - e.plen);
+                // shorter prefixes were written first; no tbl8 group exists yet
+                std::fill(t24 + start, t24 + start + cnt, e.list1);
+            } else {
+                uint32_t i24 = e.a32 >> 8;
+                uint32_t w = t24[i24];
+                uint32_t g;
+                if (w & INFW_TBL8_FLAG) {
+                    g = w & ~INFW_TBL8_FLAG;
+                } else {
+                    g = (uint32_t)(out.tbl8.size() >> 8);
+                    if (g >= INFW_TBL8_FLAG) {
+                        set_error("compile: tbl8 groups exhausted");
+                        return -ENOSPC;
+                    }
+                    out.tbl8.resize(out.tbl8.size() + 256, w);
+                    t24[i24] = INFW_TBL8_FLAG | g;
+                }
+                uint32_t start = e.a32 & 0xFFu, cnt = 1u << (32 - e.plen);
+                std::fill(out.tbl8.begin() + ((size_t)g << 8) + start,
+                          out.tbl8.begin() + ((size_t)g << 8) + start + cnt, e.list1);
+            }
+        }
+    }
+    if (out.tbl24.empty()) out.tbl24.push_back(0);
+    if (out.tbl8.empty()) out.tbl8.assign(256, 0);
+
+    // --- long prefixes: levels, markers, best-matching-prefix
+    {
+        std::vector<uint8_t> lv;
+        bool present[129] = {};
+        for (const auto &r : longs) present[r.len] = true;
+        for (int l = 33; l <= 128; l++)
+            if (present[l]) lv.push_back((uint8_t)l);
+        if (lv.size() > INFW_MAX_LEVELS) {
+            set_error("compile: too many IPv6 prefix lengths");
+            return -ENOSPC;
+        }
+        out.levels = lv;
+        int nl = (int)lv.size();
+        int level_idx[129];
+        for (int i = 0; i < 129; i++) level_idx[i] = -1;
+        for (int i = 0; i < nl; i++) level_idx[lv[i]] = i;
+
+        LongSet set;
+        set.init(longs.size() * 6 + 16);
+        for (const auto &r : longs) {
+            int t = level_idx[r.len];
+            int L = 0, R = nl - 1;
+            while (L <= R) {
+                int mid = (L + R) >> 1;
+                uint32_t len = lv[mid];
+                uint64_t h = r.hi, l = r.lo;
+                infw_mask128(len, &h, &l);
+                LongNode *n = set.find_or_insert(r.slot << 8 | len, h, l);
+                if (mid == t) {
+                    n->real = r.list1;
+                    break;
+                }
+                if (mid < t) L = mid + 1;  // marker on the way to a longer level
+                else R = mid - 1;
+            }
+        }
+        // bmp: a real node is its own answer; a marker takes the longest real
+        // prefix (of a level below it) covering its bits.
+        uint64_t cap = 1024;
+        while (cap < set.n * 2) cap <<= 1;
+        out.ltab.assign(cap, infw_long_entry{0, 0, 0, 0, {0, 0}});
+        uint64_t lmask = cap - 1;
+        for (const LongNode &n : set.tab) {
+            if (n.tag == 0) continue;
+            uint32_t bmp = n.real;
+            if (!bmp) {
+                uint32_t slot = n.tag >> 8, len = n.tag & 0xFF;
+                for (int i = level_idx[len] - 1; i >= 0 && !bmp; i--) {
+                    uint64_t h = n.hi, l = n.lo;
+                    infw_mask128(lv[i], &h, &l);
+                    const LongNode *p = set.find(slot << 8 | lv[i], h, l);
+                    if (p && p->real) bmp = p->real;
+                }
+            }
+            uint64_t i = infw_long_hash(n.tag, n.hi, n.lo) & lmask;
+            while (out.ltab[i].tag) i = (i + 1) & lmask;
+            out.ltab[i] = infw_long_entry{n.hi, n.lo, n.tag, bmp, {0, 0}};
+        }
+        out.n_long_entries = set.n;
+    }
+    return 0;
+}
+
+infw_dev_tables HostTables::view() const {
+    infw_dev_tables t;
+    memset(&t, 0, sizeof(t));
+    t.if_keys = if_keys.data();
+    t.if_slot = if_slot.data();
+    t.if_mask = (uint32_t)if_keys.size() - 1;
+    t.n_slots = n_slots;
+    t.tbl24 = tbl24.data();
+    t.tbl8 = tbl8.data();
+    t.ltab = ltab.data();
+    t.lmask = ltab.size() - 1;
+    t.desc = desc.data();
+    t.rules = rules.data();
+    t.n_levels = (uint32_t)levels.size();
+    for (size_t i = 0; i < levels.size(); i++) t.levels[i] = levels[i];
+    return t;
+}
+
+}  // namespace infw

@@ -1,0 +1,19 @@
+"""infw — MI355X-native batched ingress-firewall classifier (host side).
+
+Package layout (ingress-node-firewall_amd/):
+  csrc/     HIP kernels (classify.hip), table compiler, C ABI (include/infw.h)
+  lib/      libinfw.so (product) and libinfw_workload.so (bench/test workloads), built in-tree
+  infw/     this Python mirror of the reference's pkg/ebpf + pkg/metrics API over the C ABI
+"""
+from ._native import (BPF_ANY, BPF_EXIST, BPF_NOEXIST, F_HOST_ONLY, F_KEEP_HOST_IMAGE, LIB_PATH, MAX_TARGETS,
+                      XDP_DROP, XDP_PASS, InfwError, LpmIpKeySt, RuleStatisticsSt, RulesValSt, RuleTypeSt)
+from .core import Classifier, build_ebpf_key, key_from_fields, verdicts_from_results
+from .controller import (IngNodeFwController, IngressNodeFirewallRules, ProtocolRule, Statistics,
+                         make_rules_val)
+
+__all__ = [
+    "Classifier", "build_ebpf_key", "key_from_fields", "verdicts_from_results", "IngNodeFwController",
+    "IngressNodeFirewallRules", "ProtocolRule", "Statistics", "make_rules_val", "LpmIpKeySt", "RulesValSt",
+    "RuleTypeSt", "RuleStatisticsSt", "InfwError", "BPF_ANY", "BPF_NOEXIST", "BPF_EXIST", "F_HOST_ONLY",
+    "F_KEEP_HOST_IMAGE", "XDP_DROP", "XDP_PASS", "MAX_TARGETS", "LIB_PATH",
+]

@@ -1,0 +1,191 @@
+"""ctypes bindings of libinfw.so (include/infw.h) and libinfw_workload.so.
+
+The shared objects are built in-tree by `make` (or __graft_entry__.build()) into
+ingress-node-firewall_amd/lib/.  There is no fallback: if the library is
+missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(_PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libinfw.so")
+WL_LIB_PATH = os.path.join(LIB_DIR, "libinfw_workload.so")
+
+MAX_TARGETS = 1024
+MAX_RULES_PER_TARGET = 100
+XDP_ABORTED, XDP_DROP, XDP_PASS = 0, 1, 2
+BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
+F_HOST_ONLY = 0x1
+F_KEEP_HOST_IMAGE = 0x2
+HDR_SNAP = 80
+
+
+class LpmIpKeySt(C.Structure):
+    """struct lpm_ip_key_st (bpf/ingress_node_firewall.h:83-87), BpfLpmIpKeySt."""
+    _pack_ = 1
+    _fields_ = [("prefixLen", C.c_uint32), ("ingress_ifindex", C.c_uint32), ("ip_data", C.c_uint8 * 16)]
+
+    def tobytes(self) -> bytes:
+        return bytes(self)
+
+    def __eq__(self, other):  # reflect.DeepEqual on the Go struct == byte equality
+        return isinstance(other, LpmIpKeySt) and bytes(self) == bytes(other)
+
+    def __hash__(self):
+        return hash(bytes(self))
+
+    def __repr__(self):
+        return f"LpmIpKeySt(prefixLen={self.prefixLen}, ifindex={self.ingress_ifindex}, ip={bytes(self.ip_data).hex()})"
+
+
+class RuleTypeSt(C.Structure):
+    """struct ruleType_st (ingress_node_firewall.h:69-77), BpfRuleTypeSt, 12 B packed."""
+    _pack_ = 1
+    _fields_ = [("ruleId", C.c_uint32), ("protocol", C.c_uint8), ("dstPortStart", C.c_uint16),
+                ("dstPortEnd", C.c_uint16), ("icmpType", C.c_uint8), ("icmpCode", C.c_uint8),
+                ("action", C.c_uint8)]
+
+
+class RulesValSt(C.Structure):
+    """struct rulesVal_st (ingress_node_firewall.h:89-91), BpfRulesValSt, 1200 B."""
+    _pack_ = 1
+    _fields_ = [("rules", RuleTypeSt * MAX_RULES_PER_TARGET)]
+
+    def __eq__(self, other):
+        return isinstance(other, RulesValSt) and bytes(self) == bytes(other)
+
+    def __hash__(self):
+        return hash(bytes(self))
+
+
+class RuleStatisticsSt(C.Structure):
+    """struct ruleStatistics_st (ingress_node_firewall.h:45-54), BpfRuleStatisticsSt."""
+    _fields_ = [("allow_packets", C.c_uint64), ("allow_bytes", C.c_uint64),
+                ("deny_packets", C.c_uint64), ("deny_bytes", C.c_uint64)]
+
+
+class BatchSoa(C.Structure):
+    """struct infw_batch_soa (include/infw.h)."""
+    _fields_ = [("saddr", C.c_void_p), ("ifindex", C.c_void_p), ("pkt_len", C.c_void_p),
+                ("meta", C.c_void_p), ("l4word", C.c_void_p)]
+
+
+class TableInfo(C.Structure):
+    _fields_ = [("epoch", C.c_uint64), ("n_entries", C.c_uint64), ("n_if_slots", C.c_uint32),
+                ("n_lists", C.c_uint32), ("n_rules", C.c_uint64), ("n_tbl8_groups", C.c_uint64),
+                ("n_long_levels", C.c_uint32), ("n_long_entries", C.c_uint64),
+                ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double)]
+
+
+assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12
+assert C.sizeof(RulesValSt) == 1200 and C.sizeof(RuleStatisticsSt) == 32
+
+# Every symbol include/infw.h declares (checked by tests/test_abi_cpu.py).
+ABI_SYMBOLS = [
+    "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
+    "infw_table_delete", "infw_table_get_next_key", "infw_table_lookup", "infw_table_count",
+    "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
+    "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
+    "infw_table_info", "infw_debug_walk", "infw_last_error", "infw_abi_version",
+]
+
+
+def _load(path: str) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `make` (or __graft_entry__.build()); "
+                          "there is no non-native fallback")
+    return C.CDLL(path)
+
+
+lib = _load(LIB_PATH)
+P = C.POINTER
+_sig = {
+    "infw_create": (C.c_int, [P(C.c_void_p), P(C.c_int), C.c_int, C.c_uint32, C.c_uint32]),
+    "infw_destroy": (None, [C.c_void_p]),
+    "infw_num_devices": (C.c_int, [C.c_void_p]),
+    "infw_table_update": (C.c_int, [C.c_void_p, P(LpmIpKeySt), P(RulesValSt), C.c_uint64]),
+    "infw_table_update_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                          C.c_uint64, P(C.c_uint64)]),
+    "infw_table_delete": (C.c_int, [C.c_void_p, P(LpmIpKeySt)]),
+    "infw_table_get_next_key": (C.c_int, [C.c_void_p, P(LpmIpKeySt), P(LpmIpKeySt)]),
+    "infw_table_lookup": (C.c_int, [C.c_void_p, P(LpmIpKeySt), P(RulesValSt)]),
+    "infw_table_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "infw_table_commit": (C.c_int, [C.c_void_p]),
+    "infw_classify": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
+                                C.c_void_p]),
+    "infw_stats_read": (C.c_int, [C.c_void_p, C.c_uint32, P(RuleStatisticsSt), P(C.c_int)]),
+    "infw_stats_read_all": (C.c_int, [C.c_void_p, P(RuleStatisticsSt)]),
+    "infw_stats_reset": (C.c_int, [C.c_void_p]),
+    "infw_stats_bind": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "infw_stats_device_ptr": (C.c_int, [C.c_void_p, C.c_int, P(C.c_void_p)]),
+    "infw_build_ebpf_key": (C.c_int, [C.c_uint32, C.c_char_p, P(LpmIpKeySt)]),
+    "infw_make_rule": (C.c_int, [P(RulesValSt), C.c_uint32, C.c_char_p, C.c_char_p, C.c_uint8, C.c_uint8,
+                                 C.c_char_p]),
+    "infw_table_info": (C.c_int, [C.c_void_p, P(TableInfo)]),
+    "infw_debug_walk": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "infw_last_error": (C.c_char_p, []),
+    "infw_abi_version": (C.c_int, []),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def last_error() -> str:
+    return (lib.infw_last_error() or b"").decode(errors="replace")
+
+
+class InfwError(OSError):
+    pass
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise InfwError(-rc, f"{what}: {os.strerror(-rc)} ({last_error()})")
+    return rc
+
+
+# ---------------------------------------------------------------- workload lib
+class GenPrefix(C.Structure):
+    _fields_ = [("addr", C.c_uint8 * 16), ("ifindex", C.c_uint32), ("plen", C.c_uint8),
+                ("family", C.c_uint8), ("pad", C.c_uint8 * 2)]
+
+
+class GenParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("prefixes", C.c_void_p), ("zipf_cdf", C.c_void_p),
+                ("n_prefixes", C.c_uint32), ("hit_permille", C.c_uint32), ("v6_permille", C.c_uint32),
+                ("cross_permille", C.c_uint32), ("p_tcp", C.c_uint32), ("p_udp", C.c_uint32),
+                ("p_icmp", C.c_uint32), ("p_sctp", C.c_uint32), ("p_special", C.c_uint32),
+                ("n_special", C.c_uint32), ("special_ports", C.c_uint16 * 16), ("n_icmp", C.c_uint32),
+                ("icmp_tc", C.c_uint16 * 16), ("len_min", C.c_uint32), ("len_max", C.c_uint32),
+                ("p_nonip", C.c_uint32), ("p_trunc", C.c_uint32), ("n_ifindex", C.c_uint32),
+                ("ifindexes", C.c_uint32 * 8)]
+
+
+wl = _load(WL_LIB_PATH)
+_wsig = {
+    "infw_wl_create": (C.c_int, [P(C.c_void_p), C.c_int, C.c_uint64, C.c_uint32, C.c_uint32]),
+    "infw_wl_destroy": (None, [C.c_void_p]),
+    "infw_wl_n_entries": (C.c_uint64, [C.c_void_p]),
+    "infw_wl_keys": (C.c_void_p, [C.c_void_p]),
+    "infw_wl_val_index": (C.c_void_p, [C.c_void_p]),
+    "infw_wl_n_templates": (C.c_uint32, [C.c_void_p]),
+    "infw_wl_templates": (C.c_void_p, [C.c_void_p]),
+    "infw_wl_params": (P(GenParams), [C.c_void_p]),
+    "infw_wl_set_packet_seed": (None, [C.c_void_p, C.c_uint64]),
+    "infw_wl_frames": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_int]),
+    "infw_wl_tuples": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]),
+    "infw_wl_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "infw_wl_upload": (C.c_int, [C.c_void_p, C.c_int]),
+    "infw_wl_gen_soa": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p]),
+}
+for _name, (_res, _args) in _wsig.items():
+    _f = getattr(wl, _name)
+    _f.restype = _res
+    _f.argtypes = _args

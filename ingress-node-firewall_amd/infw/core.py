@@ -1,0 +1,195 @@
+"""Classifier context: the table map, the batched data path and the statistics map.
+
+Thin wrapper over libinfw's C ABI (include/infw.h).  Method names follow the
+cilium/ebpf *Map calls the reference's pkg/ebpf makes on
+ingress_node_firewall_table_map / ingress_node_firewall_statistics_map.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from ._native import LpmIpKeySt, RulesValSt, RuleStatisticsSt, check
+
+
+def build_ebpf_key(if_id: int, cidr: str) -> LpmIpKeySt:
+    """BuildEBPFKey (pkg/ebpf/ingress_node_firewall_loader.go:530-547)."""
+    k = LpmIpKeySt()
+    check(N.lib.infw_build_ebpf_key(C.c_uint32(if_id), cidr.encode(), C.byref(k)), f"BuildEBPFKey({cidr!r})")
+    return k
+
+
+def key_from_fields(prefix_len: int, ifindex: int, ip: bytes) -> LpmIpKeySt:
+    k = LpmIpKeySt()
+    k.prefixLen = prefix_len
+    k.ingress_ifindex = ifindex
+    b = bytes(ip)[:16]
+    C.memmove(k.ip_data, b, len(b))
+    return k
+
+
+class Classifier:
+    """One context = replicated GPU tables + one statistics slot per device.
+
+    flags=F_HOST_ONLY gives a control-plane-only context (map API, compile,
+    debug_walk) that works without a GPU; classify() then raises ENODEV.
+    """
+
+    def __init__(self, devices: Optional[Sequence[int]] = None, max_entries: int = 0, flags: int = 0):
+        self._ctx = C.c_void_p()
+        arr = (C.c_int * len(devices))(*devices) if devices else None
+        check(N.lib.infw_create(C.byref(self._ctx), arr, len(devices) if devices else 0, max_entries, flags),
+              "infw_create")
+
+    # -- lifecycle
+    def close(self):
+        if self._ctx:
+            N.lib.infw_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def num_devices(self) -> int:
+        return N.lib.infw_num_devices(self._ctx)
+
+    # -- table map (cilium Map.Update / Delete / Lookup / Iterate)
+    def update(self, key: LpmIpKeySt, val: RulesValSt, flags: int = N.BPF_ANY) -> None:
+        check(N.lib.infw_table_update(self._ctx, C.byref(key), C.byref(val), flags), "Map.Update")
+
+    def update_rc(self, key: LpmIpKeySt, val: RulesValSt, flags: int = N.BPF_ANY) -> int:
+        return N.lib.infw_table_update(self._ctx, C.byref(key), C.byref(val), flags)
+
+    def update_batch(self, keys, vals, val_index=None, flags: int = N.BPF_ANY) -> int:
+        """keys: bytes/array of n*24 B; vals: bytes/array of m*1200 B; val_index: u32[n] or None."""
+        kb = np.frombuffer(bytes(keys) if not isinstance(keys, np.ndarray) else keys.tobytes(), np.uint8)
+        vb = np.frombuffer(bytes(vals) if not isinstance(vals, np.ndarray) else vals.tobytes(), np.uint8)
+        n = kb.size // 24
+        vi = None if val_index is None else np.ascontiguousarray(val_index, dtype=np.uint32)
+        done = C.c_uint64(0)
+        rc = N.lib.infw_table_update_batch(self._ctx, kb.ctypes.data, vb.ctypes.data,
+                                           None if vi is None else vi.ctypes.data, n, flags, C.byref(done))
+        check(rc, f"Map.BatchUpdate (applied {done.value} of {n})")
+        return done.value
+
+    def update_batch_ptr(self, keys_ptr: int, vals_ptr: int, val_index_ptr: Optional[int], n: int,
+                         flags: int = N.BPF_ANY) -> int:
+        done = C.c_uint64(0)
+        check(N.lib.infw_table_update_batch(self._ctx, keys_ptr, vals_ptr, val_index_ptr, n, flags,
+                                            C.byref(done)), "Map.BatchUpdate")
+        return done.value
+
+    def delete(self, key: LpmIpKeySt) -> None:
+        check(N.lib.infw_table_delete(self._ctx, C.byref(key)), "Map.Delete")
+
+    def delete_rc(self, key: LpmIpKeySt) -> int:
+        return N.lib.infw_table_delete(self._ctx, C.byref(key))
+
+    def lookup(self, key: LpmIpKeySt) -> Optional[RulesValSt]:
+        v = RulesValSt()
+        rc = N.lib.infw_table_lookup(self._ctx, C.byref(key), C.byref(v))
+        if rc == -2:  # ENOENT
+            return None
+        check(rc, "Map.Lookup")
+        return v
+
+    def next_key(self, key: Optional[LpmIpKeySt]) -> Optional[LpmIpKeySt]:
+        nk = LpmIpKeySt()
+        rc = N.lib.infw_table_get_next_key(self._ctx, C.byref(key) if key is not None else None, C.byref(nk))
+        if rc == -2:
+            return None
+        check(rc, "Map.NextKey")
+        return nk
+
+    def iterate(self) -> Iterator[Tuple[LpmIpKeySt, RulesValSt]]:
+        """Map.Iterate(): get_next_key walk + lookup of each key (loader.go:293-296)."""
+        k = self.next_key(None)
+        while k is not None:
+            v = self.lookup(k)
+            if v is not None:
+                yield k, v
+            k = self.next_key(k)
+
+    def count(self) -> int:
+        n = C.c_uint64(0)
+        check(N.lib.infw_table_count(self._ctx, C.byref(n)), "count")
+        return n.value
+
+    def commit(self) -> None:
+        check(N.lib.infw_table_commit(self._ctx), "commit")
+
+    def info(self) -> Dict[str, float]:
+        ti = N.TableInfo()
+        check(N.lib.infw_table_info(self._ctx, C.byref(ti)), "info")
+        return {f: getattr(ti, f) for f, _ in N.TableInfo._fields_}
+
+    # -- data path
+    def classify_ptrs(self, dev: int, saddr: int, ifindex: int, pkt_len: int, meta: int, l4word: int, n: int,
+                      results: int = 0, verdicts: int = 0, stream: int = 0) -> None:
+        b = N.BatchSoa(saddr, ifindex, pkt_len, meta, l4word)
+        check(N.lib.infw_classify(self._ctx, dev, C.byref(b), n, results or None, verdicts or None,
+                                  stream or None), "classify")
+
+    def classify(self, batch, results=None, verdicts=None, dev: int = 0, stream=None) -> None:
+        """batch: infw.batch.SoaBatch (torch tensors on the device); results/verdicts: torch tensors or None.
+        stream: torch.cuda.Stream or raw hipStream_t int; default torch's current stream."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(batch.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        self.classify_ptrs(dev, batch.saddr.data_ptr(), batch.ifindex.data_ptr(), batch.pkt_len.data_ptr(),
+                           batch.meta.data_ptr(), batch.l4word.data_ptr(), batch.n,
+                           results.data_ptr() if results is not None else 0,
+                           verdicts.data_ptr() if verdicts is not None else 0, sp)
+
+    # -- statistics map
+    def stats_read(self, rule_id: int) -> List[RuleStatisticsSt]:
+        """Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt): one entry per device slot."""
+        nd = max(1, self.num_devices)
+        arr = (RuleStatisticsSt * nd)()
+        ns = C.c_int(0)
+        check(N.lib.infw_stats_read(self._ctx, rule_id, arr, C.byref(ns)), "stats_read")
+        return list(arr[: ns.value])
+
+    def stats_read_all(self) -> np.ndarray:
+        arr = (RuleStatisticsSt * N.MAX_TARGETS)()
+        check(N.lib.infw_stats_read_all(self._ctx, arr), "stats_read_all")
+        return np.frombuffer(bytes(arr), dtype=np.uint64).reshape(N.MAX_TARGETS, 4).copy()
+
+    def stats_reset(self) -> None:
+        check(N.lib.infw_stats_reset(self._ctx), "stats_reset")
+
+    def stats_bind(self, dev: int, ptr: Optional[int]) -> None:
+        check(N.lib.infw_stats_bind(self._ctx, dev, ptr or None), "stats_bind")
+
+    def stats_device_ptr(self, dev: int = 0) -> int:
+        p = C.c_void_p()
+        check(N.lib.infw_stats_device_ptr(self._ctx, dev, C.byref(p)), "stats_device_ptr")
+        return p.value
+
+    # -- verification hook (tests only)
+    def debug_walk(self, tuples: np.ndarray) -> np.ndarray:
+        t = np.ascontiguousarray(tuples, dtype=np.uint32).reshape(-1, 8)
+        out = np.zeros(t.shape[0], dtype=np.uint32)
+        check(N.lib.infw_debug_walk(self._ctx, t.ctypes.data, t.shape[0], out.ctypes.data), "debug_walk")
+        return out
+
+
+def verdicts_from_results(results: np.ndarray, meta: np.ndarray) -> np.ndarray:
+    """XDP verdict implied by a result word (kernel.c:423-456)."""
+    cap = (meta >> 24) & 0xFF
+    act = results & 0xFF
+    return np.where((cap < 14) | (act == N.XDP_DROP), N.XDP_DROP, N.XDP_PASS).astype(np.uint8)

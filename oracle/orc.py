@@ -1,0 +1,115 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/build/liborc.so (oracle/infw_oracle.c), the CPU
+restatement of bpf/ingress_node_firewall_kernel.c and of the LPM-trie map it
+runs against.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module, and only as the checker.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liborc.so")
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} not built: run `make`")
+_lib = C.CDLL(LIB_PATH)
+
+P = C.POINTER
+_sig = {
+    "orc_map_create": (C.c_void_p, [C.c_uint32]),
+    "orc_map_destroy": (None, [C.c_void_p]),
+    "orc_map_update": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint64]),
+    "orc_map_delete": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "orc_map_lookup": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p]),
+    "orc_map_get_next_key": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p]),
+    "orc_map_count": (C.c_uint64, [C.c_void_p]),
+    "orc_xdp_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                              P(C.c_uint32), P(C.c_int)]),
+    "orc_classify_frames": (C.c_double, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "orc_collect_events": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
+}
+for _n, (_r, _a) in _sig.items():
+    getattr(_lib, _n).restype = _r
+    getattr(_lib, _n).argtypes = _a
+
+STATS_DTYPE = np.uint64  # [1024, 4]: allow.packets, allow.bytes, deny.packets, deny.bytes
+
+
+class OracleMap:
+    """The table map + data path of the reference, on the CPU."""
+
+    def __init__(self, max_entries: int = 1 << 22):
+        self._m = _lib.orc_map_create(max_entries)
+
+    def close(self):
+        if self._m:
+            _lib.orc_map_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def update(self, key: bytes, val: bytes, flags: int = 0) -> int:
+        assert len(key) == 24 and len(val) == 1200
+        return _lib.orc_map_update(self._m, bytes(key), bytes(val), flags)
+
+    def delete(self, key: bytes) -> int:
+        return _lib.orc_map_delete(self._m, bytes(key))
+
+    def lookup(self, key: bytes):
+        out = C.create_string_buffer(1200)
+        rc = _lib.orc_map_lookup(self._m, bytes(key), out)
+        return None if rc else out.raw
+
+    def next_key(self, key):
+        out = C.create_string_buffer(24)
+        rc = _lib.orc_map_get_next_key(self._m, None if key is None else bytes(key), out)
+        return None if rc else out.raw
+
+    def keys(self):
+        k = self.next_key(None)
+        while k is not None:
+            yield k
+            k = self.next_key(k)
+
+    def __len__(self):
+        return int(_lib.orc_map_count(self._m))
+
+    def run(self, frame: bytes, ifindex: int, buff_len: int | None = None, stats: np.ndarray | None = None):
+        """One XDP invocation; returns (xdp_action, result_word, event_emitted)."""
+        res = C.c_uint32(0)
+        ev = C.c_int(0)
+        sp = None if stats is None else stats.ctypes.data
+        act = _lib.orc_xdp_run(self._m, sp, bytes(frame), len(frame), len(frame) if buff_len is None else buff_len,
+                               ifindex, C.byref(res), C.byref(ev))
+        return act, res.value, bool(ev.value)
+
+    def classify_frames(self, hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifindex: np.ndarray,
+                        nthreads: int = 1, want_results: bool = True):
+        """Batch over header snapshots (n x W bytes).  Returns (results, verdicts, stats[1024,4], seconds)."""
+        n = hdr.shape[0]
+        h = np.ascontiguousarray(hdr, dtype=np.uint8)
+        w = h.shape[1] if n else 0
+        offs = (np.arange(n, dtype=np.uint64) * np.uint64(w))
+        cap = np.minimum(np.ascontiguousarray(caplen, np.uint32), np.uint32(max(w, 0)))
+        # the program never reads past byte 74, so a snapshot of w >= 80 bytes stands in for the frame
+        cap_full = np.ascontiguousarray(caplen, np.uint32) if w >= 80 else cap
+        pl = np.ascontiguousarray(pkt_len, np.uint32)
+        ifx = np.ascontiguousarray(ifindex, np.uint32)
+        res = np.zeros(n, np.uint32) if want_results else None
+        ver = np.zeros(n, np.uint8) if want_results else None
+        stats = np.zeros((1024, 4), np.uint64)
+        secs = _lib.orc_classify_frames(self._m, h.ctypes.data, offs.ctypes.data, cap_full.ctypes.data,
+                                        pl.ctypes.data, ifx.ctypes.data, n,
+                                        None if res is None else res.ctypes.data,
+                                        None if ver is None else ver.ctypes.data, stats.ctypes.data, nthreads)
+        return res, ver, stats, secs
