@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpps classified at 1M prefixes x 99-100 rules (BASELINE.json metric).
+
+One step = one pass of the hot path (parse -> LPM -> first-match scan ->
+per-rule stats) over one resident batch of synthetic SoA packets per GPU, plus
+(N > 1) the RCCL all-reduce of the 1024 x 4 u64 per-rule statistics.
+
+  python bench.py [--gpus N --steps K --warmup W]       (N > 1 under torch.distributed.run)
+
+Rank 0 prints ONE JSON line.  Workload (N=1 and per GPU at N>1):
+BASELINE.json configs[2] — 1M mixed IPv4/IPv6 prefixes, BGP-like lengths,
+4 ifindexes, 4096 interned 99-rule lists, Zipf(1.1) traffic — with a
+128M-packet batch per GPU (configs[3]'s 1B-packet job is 8 x 128M).
+Packets are generated on the device from their global index, so a rank's
+shard is identical at any GPU count (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "ingress-node-firewall_amd")]
+
+ALGO_BYTES_PER_PKT = 36  # 32 B SoA tuple in + 4 B result word out
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md)
+METRIC = "Mpps classified @1M prefixes x 100 rules, 1/2/4/8 GPUs; % HBM BW roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 27, help="packets per GPU per step")
+    ap.add_argument("--cfg", type=int, default=2, choices=[1, 2, 4])
+    ap.add_argument("--prefixes", type=int, default=0, help="override table size (0 = config default)")
+    ap.add_argument("--cpu-sample", type=int, default=8 << 20, help="packets in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_cfg2.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import infw
+    from infw import workloads as W
+    from infw.batch import SoaBatch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    def log(*a):
+        if rank == 0:
+            print(*a, file=sys.stderr, flush=True)
+
+    # ---- tables (host compile, replicated on every GPU)
+    t0 = time.time()
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes)
+    clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    t1 = time.time()
+    clf.commit()
+    info = clf.info()
+    log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries loaded in {t1 - t0:.1f}s, commit {time.time() - t1:.1f}s "
+        f"(compile {info['compile_ms']:.0f} ms, upload {info['upload_ms']:.0f} ms, "
+        f"{info['device_bytes'] / 2**20:.0f} MiB/GPU, lists={info['n_lists']}, levels={info['n_long_levels']})")
+
+    # ---- resident input shard, generated on the device by global packet index
+    n = args.batch
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, start=rank * n, dev_ordinal=local)
+    results = torch.empty(n, dtype=torch.int32, device=dev)
+    stats = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # this step's per-rule counters
+    total = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # job totals (all ranks)
+    clf.stats_bind(0, stats.data_ptr())
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        stats.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        clf.classify(batch, results=results, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_reduce(stats)           # RCCL over xGMI: 32 KiB of u64 counters
+        total.add_(stats)
+
+    for _ in range(args.warmup):
+        step()
+    total.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - ts
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    total_pkts = n * world * args.steps
+    mpps = total_pkts / elapsed / 1e6
+    avg_kern_ms = sum(kern_ms) / len(kern_ms)
+    achieved = ALGO_BYTES_PER_PKT * n / (avg_kern_ms * 1e-3) / 1e9
+    counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get("hbm_bytes_per_packet", None)
+            traffic = None if traffic is None else round(traffic * n)
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(mpps, 2),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": {1: "cfg1: 10k IPv4 /16-/32 prefixes x 10 rules",
+                         2: "cfg2: 1M mixed IPv4/IPv6 prefixes (BGP-like lengths) x 99 rules/target, "
+                            "4096 interned lists, 4 ifindexes, Zipf(1.1) sources",
+                         4: "cfg4: adversarial /128 + last-slot ICMPv6"}[args.cfg],
+            "prefixes": wl.n_entries,
+            "packets_per_gpu_per_step": n,
+            "global_batch": n * world,
+            "parallelism": f"dp{world} (packet shards, replicated tables, RCCL all-reduce of stats)",
+            "packets_counted_in_stats": counted,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "kernel": "classify_kernel<true,false>",
+            "kernel_ms_avg": round(avg_kern_ms, 4),
+            "algorithmic_bytes_per_packet": ALGO_BYTES_PER_PKT,
+        },
+        "cpu_baseline": None,
+    }
+
+    # ---- CPU baseline: the oracle (plain C restatement of kernel.c) on host cores, rank 0, N=1 only
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, wl, results, n)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    clf.stats_bind(0, None)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, wl, results, n):
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    m = orc.OracleMap(max_entries=wl.n_entries + 16)
+    for k, v in wl.entries():
+        m.update(k, v)
+    s = min(args.cpu_sample, n)
+    hdr, cap, pl, ifx = wl.frames(0, s)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    res, _, _, secs = m.classify_frames(hdr, cap, pl, ifx, nthreads=threads)
+    gpu = results[:s].cpu().numpy().view(np.uint32)
+    parity = bool(np.array_equal(gpu, res))
+    return {
+        "value": round(s / secs / 1e6, 3),
+        "unit": "Mpps",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {s} packets of rank 0's cfg{args.cfg} batch, {threads} pthreads, oracle/infw_oracle.c "
+                  f"(frame parse + hash-per-length LPM + 100-slot scan), {secs:.2f}s wall",
+        "gpu_results_bitexact_on_sample": parity,
+    }
+
+
+if __name__ == "__main__":
+    main()

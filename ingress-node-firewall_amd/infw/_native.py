@@ -93,6 +93,15 @@ ABI_SYMBOLS = [
 ]
 
 
+# torch (device memory, streams, RCCL) ships its own libamdhip64.so.7; loading it
+# first makes libinfw bind to that same HIP runtime (same SONAME), so device
+# pointers and streams are shared by one runtime in the process.
+try:  # pragma: no cover - import side effect only
+    import torch as _torch  # noqa: F401
+except Exception:  # torch absent: libinfw uses /opt/rocm's runtime
+    _torch = None
+
+
 def _load(path: str) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError(f"{path} not built: run `make` (or __graft_entry__.build()); "

@@ -1,0 +1,159 @@
+"""GPU parity: the HIP classifier (through the C ABI) against the oracle.
+
+Bit-exact on result words ((ruleId & 0xFFFFFF) << 8 | action), XDP verdicts and
+the per-rule allow/deny packet/byte counters, for every BASELINE config at
+sizes the oracle finishes in seconds, plus size-independent properties at the
+bench sizes.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import infw  # noqa: E402
+from infw import workloads as W  # noqa: E402
+from infw.batch import SoaBatch  # noqa: E402
+
+from parity import assert_parity, check_cfg, gpu_run, oracle_for, stats_from_results  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.parametrize("cfg,n,npfx,ntmpl", [
+    (W.CFG0_DEMO, 1 << 20, 0, 0),            # configs[0]: demo-1 sample on 1M packets
+    (W.CFG1_V4_10K, 1 << 20, 0, 0),          # configs[1] table at full size
+    (W.CFG2_MIXED_1M, 1 << 19, 100000, 512),  # configs[2] shape, reduced table
+    (W.CFG4_ADVERSARIAL, 1 << 19, 20000, 64),
+])
+def test_parity_configs(cfg, n, npfx, ntmpl):
+    r = check_cfg(cfg, n, npfx, ntmpl)
+    assert_parity(r, f"cfg{cfg}")
+    # the workload must exercise the path: matches of both actions
+    acts = np.bincount(r["ores"] & 0xFF, minlength=3)
+    assert acts[1] + acts[2] > 0
+
+
+def test_parity_cfg2_full_table_subsample():
+    """configs[2] at its full 1M-prefix table, 256k packets from the middle of a shard."""
+    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, start=(1 << 27) + 12345)
+    assert_parity(r, "cfg2-full")
+
+
+def test_ragged_and_empty_batches():
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=128)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    for n in (0, 1, 63, 64, 65, 255, 257, 1000, 4097):
+        batch = SoaBatch.empty(max(n, 1), dev).slice(0, n)
+        if n:
+            wl.gen_device(batch, 777, 0)
+        clf.stats_reset()
+        gres, gver = gpu_run(clf, batch, n)
+        hdr, cap, pl, ifx = wl.frames(777, n)
+        ores, over, ostats, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=2)
+        assert np.array_equal(gres, ores), n
+        assert np.array_equal(gver, over), n
+        assert np.array_equal(clf.stats_read_all(), ostats), n
+
+
+def test_ipv4_ignores_saddr_tail_and_stats_accumulate():
+    """IPv4 keys use only ip_data[0..3] (kernel.c:207-212): garbage in bytes 4..15 changes nothing;
+    counters accumulate across batches like the per-CPU map (no reset between runs)."""
+    r = check_cfg(W.CFG1_V4_10K, 1 << 16)
+    batch, clf = r["batch"], r["clf"]
+    b2 = SoaBatch(batch.saddr.clone(), batch.ifindex, batch.pkt_len, batch.meta, batch.l4word)
+    b2.saddr[:, 4:] = torch.randint(0, 256, (batch.n, 12), dtype=torch.uint8, device=batch.device)
+    v4 = (batch.meta & 0xFFFF) == 0x0800
+    b2.saddr[~v4] = batch.saddr[~v4]
+    gres2, _ = gpu_run(clf, b2, batch.n)
+    assert np.array_equal(gres2, r["ores"])
+    assert np.array_equal(clf.stats_read_all(), 2 * r["ostats"])
+
+
+def test_epoch_swap_between_batches():
+    """configs[4]: live table swap mid-stream — batch A on epoch 1, commit, batch B on epoch 2;
+    the oracle applies the identical key updates between the same two batches."""
+    wl = W.Workload(W.CFG4_ADVERSARIAL, n_prefixes=20000, n_templates=64)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 64)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 1 << 18
+    clf.stats_reset()
+    a = SoaBatch.empty(n, dev)
+    wl.gen_device(a, 0, 0)
+    gres_a, _ = gpu_run(clf, a, n)
+    hdr, cap, pl, ifx = wl.frames(0, n)
+    ores_a, _, ost_a, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(gres_a, ores_a)
+    # swap: delete every 3rd key, rewrite every 5th with another template, add /128 overrides
+    keys = wl.keys_bytes().reshape(-1, 24)
+    tmpl = wl.templates_bytes().reshape(-1, 1200)
+    for i in range(0, keys.shape[0], 3):
+        kb = keys[i].tobytes()
+        rc1 = clf.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb))
+        rc2 = m.delete(kb)
+        assert rc1 == rc2
+    for i in range(1, keys.shape[0], 5):
+        kb, vb = keys[i].tobytes(), tmpl[(i * 7) % tmpl.shape[0]].tobytes()
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vb)) == \
+            m.update(kb, vb)
+    clf.commit()
+    b = SoaBatch.empty(n, dev)
+    wl.gen_device(b, n, 0)
+    gres_b, _ = gpu_run(clf, b, n)
+    hdr, cap, pl, ifx = wl.frames(n, n)
+    ores_b, _, ost_b, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(gres_b, ores_b)
+    assert np.array_equal(clf.stats_read_all(), ost_a + ost_b)  # stats persist across swaps
+
+
+def test_full_size_properties():
+    """configs[2] at the bench size (128M packets, full table): size-independent properties —
+    per-rule counters == counters implied by the result words; two runs identical; the first
+    and last 64k packets bit-exact against the oracle."""
+    n = 1 << 27
+    wl = W.Workload(W.CFG2_MIXED_1M)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    dev = torch.device("cuda", 0)
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 0, 0)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    stats = torch.zeros((1024, 4), dtype=torch.int64, device=dev)
+    clf.stats_bind(0, stats.data_ptr())
+    clf.classify(batch, results=res)
+    torch.cuda.synchronize()
+    res1 = res.clone()
+    # counters implied by result words, computed with torch on the device
+    r = res.to(torch.int64) & 0xFFFFFFFF
+    act, key = r & 0xFF, (r >> 8) & 0xFFFF
+    plen = batch.pkt_len.to(torch.int64)
+    want = torch.zeros((1024, 4), dtype=torch.int64, device=dev)
+    for a, col in ((2, 0), (1, 2)):
+        sel = (act == a) & (key < 1024)
+        want[:, col] = torch.bincount(key[sel], minlength=1024)
+        want[:, col + 1] = torch.zeros(1024, dtype=torch.int64, device=dev).index_add_(0, key[sel], plen[sel])
+    assert torch.equal(stats, want)
+    clf.classify(batch, results=res)
+    torch.cuda.synchronize()
+    assert torch.equal(res, res1)
+    assert torch.equal(stats, 2 * want)
+    clf.stats_bind(0, None)
+    m = oracle_for(wl)
+    for start in (0, n - (1 << 16)):
+        hdr, cap, pl, ifx = wl.frames(start, 1 << 16)
+        ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+        got = res1[start:start + (1 << 16)].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, ores), start
