@@ -1,0 +1,181 @@
+"""Golden vectors from the reference's own tests and the survey's probe records.
+
+Each vector runs through (1) the oracle (pins the oracle) and (2) the
+product's control plane + table compiler on a host-only context, walking the
+compiled GPU table image on the CPU (infw_debug_walk).  The same vectors run
+through the HIP kernel in test_gpu_golden.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import goenc
+import infw
+import orc
+from frames import frame, snapshots
+from infw import workloads as W
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return json.load(open(os.path.join(GOLD, name)))
+
+
+def probe_frames(case):
+    fr, ifx = [], []
+    for p in case["packets"]:
+        fr.append(frame(p["src"], proto=p.get("proto", "tcp"), dport=p.get("dport", 0),
+                        icmp_type=p.get("icmp_type", 0), icmp_code=p.get("icmp_code", 0),
+                        ethertype=p.get("ethertype"), ihl=p.get("ihl", 5), truncate=p.get("truncate")))
+        ifx.append(p["ifindex"])
+    return fr, ifx
+
+
+def expected_stats(case, frames):
+    st = np.zeros((1024, 4), np.uint64)
+    for p, f in zip(case["packets"], frames):
+        for rid, kind in p["expect"]["stats"]:
+            c = 0 if kind == "allow" else 2
+            st[rid, c] += 1
+            st[rid, c + 1] += len(f)
+    return st
+
+
+@pytest.mark.parametrize("case", load("survey_probes.json")["cases"], ids=lambda c: c["name"][:50])
+def test_survey_probes_oracle(case):
+    m = orc.OracleMap()
+    for e in case["table"]:
+        assert m.update(goenc.build_key(e["key"]["ifindex"], e["key"]["cidr"]), goenc.raw_value(e["rules"])) == 0
+    if "expect_entries" in case:
+        assert len(m) == case["expect_entries"]
+    frames, ifx = probe_frames(case)
+    stats = np.zeros((1024, 4), np.uint64)
+    for p, f, i in zip(case["packets"], frames, ifx):
+        act, res, _ = m.run(f, i, stats=stats)
+        assert act == p["expect"]["retval"], (p, act, hex(res))
+        if "result" in p["expect"]:
+            assert res == p["expect"]["result"]
+    assert np.array_equal(stats, expected_stats(case, frames))
+
+
+@pytest.mark.parametrize("case", load("survey_probes.json")["cases"], ids=lambda c: c["name"][:50])
+def test_survey_probes_compiled_tables(case):
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    for e in case["table"]:
+        c.update(infw.build_ebpf_key(e["key"]["ifindex"], e["key"]["cidr"]),
+                 infw.RulesValSt.from_buffer_copy(goenc.raw_value(e["rules"])))
+    c.commit()
+    if "expect_entries" in case:
+        assert c.count() == case["expect_entries"]
+    frames, ifx = probe_frames(case)
+    hdr, cap, pl = snapshots(frames)
+    res = c.debug_walk(W.pack_frames(hdr, cap, pl, np.array(ifx, np.uint32)))
+    tuples = W.pack_frames(hdr, cap, pl, np.array(ifx, np.uint32))
+    ver = infw.verdicts_from_results(res, tuples[:, 6])
+    for p, v, r in zip(case["packets"], ver, res):
+        assert v == p["expect"]["retval"], (p, v, hex(r))
+        if "result" in p["expect"]:
+            assert r == p["expect"]["result"]
+    # counters implied by the result words equal the probe's counters
+    from parity import stats_from_results
+    assert np.array_equal(stats_from_results(res, pl), expected_stats(case, frames))
+
+
+def http_targets(doc, tc):
+    """(frame, ifindex, expected XDP action) for each connection of a test case."""
+    out = []
+    for target, ok in tc["targetResult"].items():
+        ip, port = target.split(":")
+        last = int(ip.split(".")[-1])
+        i = (last - 1) // 4                       # 192.0.2.{4i+1} is dummy{i}
+        peer = f"192.0.2.{4 * i + 2}"
+        out.append((frame(peer, ip, "tcp", int(port)), doc["ifindex"][f"dummy{i}"], 2 if ok else 1))
+    return out
+
+
+def test_ebpfsyncer_http_oracle():
+    """TestSyncInterfaceIngressRulesWithHTTP: sync sequence + connection verdicts, on the oracle."""
+    doc = load("ref_ebpfsyncer_http.json")
+    m = orc.OracleMap()
+    for tc in doc["test_cases"]:
+        goenc.sync(m, {} if tc["isDelete"] else goenc.desired(tc["rules"], doc["ifindex"]))
+        for f, ifx, want in http_targets(doc, tc):
+            act, res, _ = m.run(f, ifx)
+            assert act == want, (tc["name"], ifx, hex(res))
+
+
+def test_ebpfsyncer_http_product_controller():
+    """The same sequence through the product's loader mirror (IngNodeFwController over the C ABI)."""
+    doc = load("ref_ebpfsyncer_http.json")
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    ctl = infw.IngNodeFwController(c, if_indices=lambda name: [doc["ifindex"][name]])
+    for tc in doc["test_cases"]:
+        if tc["isDelete"]:
+            ctl.reset_all()
+        else:
+            rules = {name: [infw.IngressNodeFirewallRules(e["source_cidrs"], [infw.ProtocolRule(**r) for r in
+                                                                            e["rules"]]) for e in ents]
+                     for name, ents in (tc["rules"] or {}).items()}
+            ctl.ingress_node_fw_rules_loader(rules)
+        tg = http_targets(doc, tc)
+        hdr, cap, pl = snapshots([t[0] for t in tg])
+        tuples = W.pack_frames(hdr, cap, pl, np.array([t[1] for t in tg], np.uint32))
+        ver = infw.verdicts_from_results(c.debug_walk(tuples), tuples[:, 6])
+        assert list(ver) == [t[2] for t in tg], tc["name"]
+
+
+def test_ebpfsyncer_key_sets():
+    """TestVerifyBPFKeysAfterInterfaceIngressRulesUpdate: the map's key set after each sync."""
+    doc = load("ref_ebpfsyncer_keys.json")
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    ctl = infw.IngNodeFwController(c, if_indices=lambda name: [doc["ifindex"][name]])
+    m = orc.OracleMap()
+    for tc in doc["test_cases"]:
+        if tc["isDelete"]:
+            ctl.reset_all()
+            goenc.sync(m, {})
+        else:
+            rules = {name: [infw.IngressNodeFirewallRules(e["source_cidrs"], [infw.ProtocolRule(**r) for r in
+                                                                            e["rules"]]) for e in ents]
+                     for name, ents in (tc["rules"] or {}).items()}
+            ctl.ingress_node_fw_rules_loader(rules)
+            goenc.sync(m, goenc.desired(tc["rules"], doc["ifindex"]))
+        want = {goenc.build_key(doc["ifindex"][i], cidr) for i, cidr in tc["expectedKeys"]}
+        got = set(ctl.get_bpf_map_content_for_test().keys())
+        assert got == want, tc["name"]
+        assert set(m.keys()) == want, tc["name"]
+
+
+def test_loader_key_identity():
+    """TestAddOrUpdateRules: distinct (ifindex, prefix) pairs are distinct keys."""
+    for tc in load("ref_loader_keys.json")["test_cases"]:
+        c = infw.Classifier(flags=infw.F_HOST_ONLY)
+        m = orc.OracleMap()
+        val = goenc.raw_value([{"slot": 0, "ruleId": tc["rule"]["ruleId"], "protocol": 0, "dstPortStart": 0,
+                                "dstPortEnd": 0, "icmpType": 0, "icmpCode": 0, "action": tc["rule"]["action"]}])
+        for ifx, cidr in tc["keys"]:
+            k = infw.build_ebpf_key(ifx, cidr)
+            assert bytes(k) == goenc.build_key(ifx, cidr)
+            c.update(k, infw.RulesValSt.from_buffer_copy(val))
+            assert m.update(bytes(k), val) == 0
+        assert c.count() == tc["expected_n_keys"] == len(m)
+
+
+def test_demo1_sample():
+    """configs[0]: config/samples/ingressnodefirewall-demo-1.yaml ingress[0] (TCP 100-200 Allow, UDP 8000 Allow)."""
+    m = orc.OracleMap()
+    rules = [{"order": 10, "protocol": "TCP", "ports": "100-200", "action": "Allow"},
+             {"order": 20, "protocol": "UDP", "ports": 8000, "action": "Allow"}]
+    for cidr in ("1.1.1.1/24", "100:1::1/64"):
+        assert m.update(goenc.build_key(1, cidr), goenc.make_value(rules)) == 0
+    cases = [("1.1.1.9", "tcp", 100, 2, (10 << 8) | 2), ("1.1.1.9", "tcp", 199, 2, (10 << 8) | 2),
+             ("1.1.1.9", "tcp", 200, 2, 0), ("1.1.1.9", "udp", 8000, 2, (20 << 8) | 2),
+             ("1.1.1.9", "udp", 8001, 2, 0), ("1.1.2.9", "tcp", 150, 2, 0),
+             ("100:1::77", "tcp", 150, 2, (10 << 8) | 2), ("100:1:0:1::77", "tcp", 150, 2, 0),
+             ("100:1::77", "icmpv6", 0, 2, 0)]
+    for src, proto, port, act, res in cases:
+        a, r, _ = m.run(frame(src, proto=proto, dport=port), 1)
+        assert (a, r) == (act, res), (src, proto, port)
