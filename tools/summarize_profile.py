@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
+
+Copies the rocprofv3 --stats summaries and writes summary.json with, for the
+classify kernel: average duration (kernel trace), per-launch PMC values, and
+the HBM traffic per launch corrected as MI355X_MICROARCH.md §HBM prescribes:
+  FETCH_SIZE, WRITE_SIZE are in KiB; FETCH_SIZE reads exactly half the bytes of
+  a wide coalesced streaming read (gfx950), exact for other shapes only after
+  calibration.  The classify kernel's streamed input is known exactly
+  (32 B/packet), so   read_bytes = FETCH_SIZE*1024 + 0.5 * 32 * n_packets
+  (the un-counted half of the stream); gathers are taken at face value
+  (64-B requests).  The uncorrected value is kept beside it.
+Also writes profiles/traffic_cfg2.json (bytes per packet) that bench.py reads.
+Usage: tools/summarize_profile.py <tag> [n_packets]
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 27
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    for f in ("kt/kt_kernel_stats.csv", "kt/kt_domain_stats.csv"):
+        p = os.path.join(src, f)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, os.path.basename(p)))
+    out = {"tag": tag, "packets_per_launch": n, "kernels": {}}
+    stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
+    for r in stats:
+        if "classify" in r["Name"]:
+            out["kernels"][r["Name"][:80]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                              "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+    pmc = collections.defaultdict(list)
+    for name in sorted(os.listdir(src)):
+        p = os.path.join(src, name, f"{name}_counter_collection.csv")
+        if not name.startswith("pmc") or not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            if "classify" in r["Kernel_Name"]:
+                pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    avg = {k: sum(v) / len(v) for k, v in pmc.items()}
+    out["pmc_avg_per_launch"] = avg
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        corr = avg["FETCH_SIZE"] * 1024 + 0.5 * 32 * n + avg["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch_raw"] = raw
+        out["hbm_bytes_per_launch"] = corr
+        out["hbm_bytes_per_packet"] = corr / n
+        out["hbm_bytes_per_packet_raw"] = raw / n
+        json.dump({"tag": tag, "hbm_bytes_per_packet": corr / n, "hbm_bytes_per_packet_raw": raw / n,
+                   "note": "classify kernel, cfg2 bench config; see profiles/%s/summary.json" % tag},
+                  open(os.path.join(ROOT, "profiles", "traffic_cfg2.json"), "w"), indent=1)
+    if "TCC_HIT_sum" in avg:
+        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+        out["l2_misses_per_packet"] = avg["TCC_MISS_sum"] / n
+    if "SQ_LDS_BANK_CONFLICT" in avg:
+        out["lds_bank_conflict_rate"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"])
+    if "GRBM_GUI_ACTIVE" in avg and out["kernels"]:
+        k = next(iter(out["kernels"].values()))
+        out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
+    bench = os.path.join(src, "kt.stdout")
+    if os.path.exists(bench):
+        lines = [l for l in open(bench) if l.startswith("{")]
+        if lines:
+            out["bench_line_under_kernel_trace"] = json.loads(lines[-1])
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "bench_line_under_kernel_trace"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
