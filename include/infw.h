@@ -194,6 +194,13 @@ int infw_table_commit(infw_ctx *ctx);
 int infw_classify(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
                   uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
 
+/* Launch shape of the classify kernel (tuning; defaults 512 / 0 / 4, or the  */
+/* INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU environment variables):    */
+/* block 256|512 threads; scan_group 0 = first-match decision tables, or    */
+/* 1|4|8 = one-lane-per-rule ballot scan with that many packets in flight; */
+/* blocks_per_cu resident workgroups per CU.                                  */
+int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
+
 /* ------------------------------------------------------------------------ */
 /* Statistics — ingress_node_firewall_statistics_map (kernel.c:36-41,        */
 /* PERCPU_ARRAY[1024] of ruleStatistics_st).  One slot per device plays the  */
@@ -245,6 +252,8 @@ struct infw_table_info {
     uint64_t device_bytes;     /* table bytes resident per device             */
     double compile_ms;         /* host compile time of the last commit        */
     double upload_ms;          /* H2D time of the last commit                 */
+    uint64_t n_v6_groups;      /* (ifindex, /32) groups of IPv6 long prefixes */
+    uint64_t n_v6_overflow;    /* groups with > 3 long prefixes (Waldvogel)   */
 };
 int infw_table_info(infw_ctx *ctx, struct infw_table_info *info);
 /* Verification hook for tests/ only — never called by infw_classify: walks     */

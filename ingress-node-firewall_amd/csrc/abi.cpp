@@ -3,6 +3,8 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -10,8 +12,8 @@
 #include "infw_internal.h"
 
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
-                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats,
-                                    uint32_t grid, hipStream_t stream);
+                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
+                                    int block, int group, int blocks_per_cu, hipStream_t stream);
 
 namespace infw {
 
@@ -56,7 +58,7 @@ struct DeviceEpoch {
 
 struct Device {
     int ordinal = 0;
-    uint32_t grid = 2048;
+    uint32_t cus = 256;
     uint64_t *stats_own = nullptr;
     uint64_t *stats = nullptr;
     std::shared_ptr<DeviceEpoch> epoch;
@@ -72,6 +74,8 @@ struct infw_ctx {
     PendingMap map;
     std::unique_ptr<HostTables> host_image;  // INFW_F_HOST_ONLY / INFW_F_KEEP_HOST_IMAGE
     std::mutex epoch_mu;  // guards devs[*].epoch swaps vs classify snapshots
+    // launch shape of the classify kernel (infw_set_launch / INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU)
+    int block = 512, group = 0, blocks_per_cu = 4;
     uint64_t epoch_no = 0;
     uint64_t committed_gen = ~0ull;
     struct infw_table_info info{};
@@ -103,14 +107,15 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
     int rc = 0;
     if ((rc = upload(*ep, h.if_keys, &t.if_keys)) || (rc = upload(*ep, h.if_slot, &t.if_slot)) ||
         (rc = upload(*ep, h.tbl24, &t.tbl24)) || (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
-        (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
-        (rc = upload(*ep, h.rules, &t.rules)))
+        (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.btab, &t.btab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
+        (rc = upload(*ep, h.rules, &t.rules)) ||
+        (rc = upload(*ep, h.ddesc, &t.ddesc)) || (rc = upload(*ep, h.dt, &t.dt)) || (rc = upload(*ep, h.levels, &t.levels)))
         return rc;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;
+    t.bmask = h.btab.size() - 1;
     t.n_levels = (uint32_t)h.levels.size();
-    for (size_t i = 0; i < h.levels.size(); i++) t.levels[i] = h.levels[i];
     out = ep;
     return 0;
 }
@@ -135,6 +140,13 @@ int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_
         *out = ctx.release();
         return 0;
     }
+    if (const char *e = getenv("INFW_BLOCK")) ctx->block = atoi(e) == 256 ? 256 : 512;
+    if (const char *e = getenv("INFW_SCAN_GROUP")) {
+        int g = atoi(e);
+        ctx->group = (g == 1 || g == 4 || g == 8) ? g : 0;
+    }
+    ctx->blocks_per_cu = ctx->block == 512 ? 4 : 6;  // 24 KiB LDS per workgroup: 32 / 24 waves per CU
+    if (const char *e = getenv("INFW_BLOCKS_PER_CU")) ctx->blocks_per_cu = atoi(e) > 0 ? atoi(e) : ctx->blocks_per_cu;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         set_error("no HIP device visible: the classifier has no CPU fallback");
@@ -164,7 +176,7 @@ int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_
         }
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o);
-        d.grid = (uint32_t)cus * 6;  // 24 KiB LDS/workgroup -> 6 resident per CU
+        d.cus = (uint32_t)cus;
         HIP_OK(hipMalloc(&d.stats_own, INFW_MAX_TARGETS * sizeof(ruleStatistics_st)));
         HIP_OK(hipMemset(d.stats_own, 0, INFW_MAX_TARGETS * sizeof(ruleStatistics_st)));
         d.stats = d.stats_own;
@@ -267,6 +279,8 @@ int infw_table_commit(infw_ctx *ctx) {
     in.device_bytes = eps.empty() ? 0 : eps[0]->bytes;
     in.compile_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    in.n_v6_groups = h.n_buckets;
+    in.n_v6_overflow = h.n_overflow_groups;
     ctx->committed_gen = ctx->map.generation;
     if (ctx->flags & (INFW_F_HOST_ONLY | INFW_F_KEEP_HOST_IMAGE))
         ctx->host_image.reset(new HostTables(std::move(h)));
@@ -287,7 +301,15 @@ int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t 
         int pk = infw_parse(q[6], q[7], &cls, &val);
         if (pk >= INFW_PK_V4) {
             uint32_t l1 = infw_lpm(t, pk, q[4], q);
-            if (l1) result = infw_scan_serial(t, t.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls], val);
+            if (l1) {
+                const uint64_t row = (uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls;
+                result = infw_dt_eval(t, t.ddesc[row], val);
+                const uint32_t scan = infw_scan_serial(t, t.desc[row], val);
+                if (scan != result) {
+                    set_error("debug_walk: decision table disagrees with the rule scan");
+                    return -EIO;
+                }
+            }
         }
         out[i] = result;
     }
@@ -327,12 +349,22 @@ int infw_classify(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n,
         set_error("hipSetDevice failed");
         return -ENODEV;
     }
-    int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.grid,
-                                  static_cast<hipStream_t>(stream));
+    int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.cus, ctx->block,
+                                  ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream));
     if (rc) {
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
+    return 0;
+}
+
+int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu) {
+    if (!ctx || (block != 256 && block != 512) || (scan_group != 0 && scan_group != 1 && scan_group != 4 && scan_group != 8) ||
+        blocks_per_cu < 1 || blocks_per_cu > 32)
+        return -EINVAL;
+    ctx->block = block;
+    ctx->group = scan_group;
+    ctx->blocks_per_cu = blocks_per_cu;
     return 0;
 }
 

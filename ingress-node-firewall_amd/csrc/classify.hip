@@ -1,51 +1,104 @@
 // classify.hip — gfx950 kernel for the batched XDP classification
 // (bpf/ingress_node_firewall_kernel.c:412-457 over one SoA batch).
 //
-// One workgroup = 4 waves x 64 lanes; a persistent grid strides over the
-// batch 256 packets at a time.  Per tile:
+// A persistent grid of kBlock-thread workgroups strides over the batch one
+// tile (kBlock packets, one per lane) at a time.  Per tile:
 //   1. each lane loads one 32-B tuple (five coalesced streams), parses it
 //      (infw_parse) and walks the LPM (ifindex hash -> IPv6 long table ->
-//      DIR-24-8), then gathers its rule-list descriptor for its class;
-//   2. the wave resolves first-match cooperatively, one lane per rule: for
-//      each lane j that needs a scan (s_ff1 over a ballot), the 64 lanes load
-//      64 consecutive rule records of j's class list, test lo <= v_j <= hi,
-//      and __ballot/ffs picks the first match — the reference's in-order scan
-//      (kernel.c:222-258) in one wave step per 64 rules;
-//   3. result words and verdicts are stored coalesced; allow/deny counters
+//      DIR-24-8), then gathers the rule-list descriptor of its packet class;
+//   2. the wave resolves first-match cooperatively, one lane per rule: it takes
+//      the lanes that need a scan G at a time (s_ff1 over a ballot), issues the
+//      G packets' 64-rule chunk loads back to back (G loads in flight instead
+//      of one dependent round trip per packet), then for each packet tests
+//      lo <= v <= hi on all 64 lanes and __ballot/ffs picks the first match —
+//      the reference's in-order scan (kernel.c:222-258) in one wave step per
+//      64 rules;
+//   3. result words / verdicts are stored coalesced; allow/deny counters
 //      accumulate in LDS (u32 packets, u64 bytes per rule id) and are flushed
 //      with one u64 atomic per touched counter when the workgroup retires.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/infw.h"
 #include "infw_tables.h"
 
 namespace {
 
-constexpr int kBlock = 256;
 constexpr int kStatKeys = INFW_MAX_TARGETS;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kIfLds = 256;  // ifindex map entries mirrored in LDS
 
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
-template <bool kResults, bool kVerdicts>
-__global__ __launch_bounds__(kBlock) void classify_kernel(const infw_dev_tables T,
-                                                          const infw_batch_soa in, uint64_t n,
-                                                          uint32_t *__restrict__ results,
+__device__ __forceinline__ bool rec_match(uint64_t rec, uint32_t v) {
+    const uint32_t lo = (uint32_t)rec & 0xFFFFu, hi = (uint32_t)(rec >> 16) & 0xFFFFu;
+    return lo <= v && v <= hi;
+}
+
+// First match of a class list (o, c) against v, starting at rule `from`, one lane per rule.
+__device__ __forceinline__ uint32_t scan_tail(const uint64_t *__restrict__ rules, uint32_t o, uint32_t c,
+                                              uint32_t v, uint32_t from, int lane) {
+    for (uint32_t k0 = from; k0 < c; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        uint64_t rec = 0;
+        bool m = false;
+        if (k < c) {
+            rec = rules[(uint64_t)o + k];
+            m = rec_match(rec, v);
+        }
+        const uint64_t mb = __ballot(m);
+        if (mb) return readlane((uint32_t)(rec >> 32), __builtin_ctzll(mb));
+    }
+    return 0;
+}
+
+// First-match result from a decision table (infw_tables.h), one lane per packet:
+// <= 3 dependent 16-B node loads (8 u16 keys each) and one result load.
+__device__ __forceinline__ uint32_t dt_eval(const uint32_t *__restrict__ dt, uint64_t dd, uint32_t v) {
+    const uint32_t S = (uint32_t)(dd >> 32) & 0xFFFFu;
+    if (S <= 1) return S ? (uint32_t)dd : 0u;
+    const uint32_t d = (uint32_t)(dd >> 48) & 0xFFu;
+    const uint4 *base = reinterpret_cast<const uint4 *>(dt) + (uint32_t)dd;
+    uint32_t node = 0, lvl = 0, span = d == 1 ? 9u : d == 2 ? 81u : 729u;
+    for (uint32_t l = 0; l < d; l++) {
+        const uint4 k = base[lvl + node];
+        const uint32_t c = infw_count_lt(k.x, v) + infw_count_lt(k.y, v) + infw_count_lt(k.z, v) +
+                           infw_count_lt(k.w, v);
+        lvl += (S + span - 1) / span;
+        span /= 9u;
+        node = node * 9u + c;
+    }
+    return reinterpret_cast<const uint32_t *>(base + lvl)[node];
+}
+
+// G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
+template <int kBlock, int G, int kAblate = 0>
+__global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
+                                                          uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats) {
     __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
     __shared__ unsigned long long s_by[2 * kStatKeys];
+    __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
     for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) {
         s_pk[i] = 0;
         s_by[i] = 0;
     }
+    const bool if_in_lds = T.if_mask < kIfLds;
+    if (if_in_lds)
+        for (uint32_t i = threadIdx.x; i <= T.if_mask; i += kBlock) {
+            s_ifk[i] = T.if_keys[i];
+            s_ifs[i] = T.if_slot[i];
+        }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const uint4 *sa4 = reinterpret_cast<const uint4 *>(in.saddr);
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t *__restrict__ rules = T.rules;
 
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
         const uint64_t i = base + threadIdx.x;
@@ -53,58 +106,109 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const infw_dev_tables 
         uint32_t meta = 0, l4w = 0, ifx = 0, plen = 0;
         uint4 sa = make_uint4(0, 0, 0, 0);
         if (valid) {
-            meta = in.meta[i];
-            l4w = in.l4word[i];
-            ifx = in.ifindex[i];
-            plen = in.pkt_len[i];
-            sa = sa4[i];
+            if (!(kAblate & 16)) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL (16: plain, diagnostic)
+                meta = __builtin_nontemporal_load(&in.meta[i]);
+                l4w = __builtin_nontemporal_load(&in.l4word[i]);
+                ifx = __builtin_nontemporal_load(&in.ifindex[i]);
+                plen = __builtin_nontemporal_load(&in.pkt_len[i]);
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(sa4) + i);
+                sa = make_uint4(t[0], t[1], t[2], t[3]);
+            } else {
+                meta = in.meta[i];
+                l4w = in.l4word[i];
+                ifx = in.ifindex[i];
+                plen = in.pkt_len[i];
+                sa = sa4[i];
+            }
         }
         int cls = 0;
         uint32_t val = 0;
-        int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
+        const int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
         uint64_t d = 0;
+        if (kAblate & 8) {  // diagnostic: input stream + output only
+            if (valid && results) results[i] = meta ^ l4w ^ sa.x ^ sa.y ^ sa.z ^ sa.w ^ ifx ^ plen;
+            continue;
+        }
         if (pk >= INFW_PK_V4) {
             const uint32_t sw[4] = {sa.x, sa.y, sa.z, sa.w};
-            uint32_t l1 = infw_lpm(T, pk, ifx, sw);
-            if (l1) d = T.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
+            uint32_t l1 = 1;  // diagnostic 1: no LPM walk, every parsed packet uses list 0
+            if (!(kAblate & 1)) {
+                // ifindex -> slot (LDS copy of the open-addressed map)
+                int slot;
+                if (if_in_lds) {
+                    uint32_t h = infw_if_hash(ifx) & T.if_mask;
+                    for (;;) {
+                        const uint32_t sl = s_ifs[h];
+                        if (sl == INFW_IF_EMPTY) { slot = -1; break; }
+                        if (s_ifk[h] == ifx) { slot = (int)sl; break; }
+                        h = (h + 1) & T.if_mask;
+                    }
+                } else {
+                    slot = infw_if_slot(T, ifx);
+                }
+                l1 = 0;
+                if (slot >= 0) {
+                    const uint32_t a32 = infw_bswap32(sa.x);
+                    // the short-table word is fetched for every packet, alongside the
+                    // IPv6 bucket probe: IPv4 and IPv6 lanes issue their misses together
+                    const uint32_t e24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+                    uint32_t lng = 0;
+                    if (pk == INFW_PK_V6 && T.n_levels) lng = infw_v6_long(T, (uint32_t)slot, a32, sw);
+                    l1 = lng;
+                    if (!lng) l1 = (e24 & INFW_TBL8_FLAG) ? T.tbl8[((uint64_t)(e24 & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu)] : e24;
+                }
+            }
+            if (l1) d = (G == 0 ? T.ddesc : T.desc)[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
         }
         const uint32_t off = (uint32_t)d, cnt = (uint32_t)(d >> 32);
 
-        // ---- first match, one lane per rule
         uint32_t result = 0;
-        uint64_t pending = __ballot(cnt != 0);
-        while (pending) {
-            const int j = __builtin_ctzll(pending);
-            pending &= pending - 1;
-            const uint32_t oj = readlane(off, j), cj = readlane(cnt, j), vj = readlane(val, j);
-            uint32_t r = 0;
-            for (uint32_t k0 = 0; k0 < cj; k0 += 64) {
-                const uint32_t k = k0 + lane;
-                uint64_t rec = 0;
-                bool m = false;
-                if (k < cj) {
-                    rec = T.rules[(uint64_t)oj + k];
-                    const uint32_t lo = (uint32_t)rec & 0xFFFFu, hi = (uint32_t)(rec >> 16) & 0xFFFFu;
-                    m = lo <= vj && vj <= hi;
-                }
-                const uint64_t mb = __ballot(m);
-                if (mb) {
-                    r = readlane((uint32_t)(rec >> 32), __builtin_ctzll(mb));
-                    break;
+        if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32);  // diagnostic 2: no first-match stage
+        else if (G == 0 && d) result = dt_eval(T.dt, d, val);
+        // ---- first match, one lane per rule, G packets in flight
+        uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
+        while (G > 0 && pending) {
+            constexpr int GG = G > 0 ? G : 1;
+            int j[GG];
+            uint32_t o[GG], c[GG], v[GG];
+            uint64_t rec[GG];
+#pragma unroll
+            for (int g = 0; g < GG; g++) {
+                if (pending) {
+                    j[g] = __builtin_ctzll(pending);
+                    pending &= pending - 1;
+                    o[g] = readlane(off, j[g]);
+                    c[g] = readlane(cnt, j[g]);
+                    v[g] = readlane(val, j[g]);
+                } else {
+                    j[g] = -1;
+                    o[g] = c[g] = v[g] = 0;
                 }
             }
-            if (lane == j) result = r;
+#pragma unroll
+            for (int g = 0; g < GG; g++) rec[g] = (uint32_t)lane < c[g] ? rules[(uint64_t)o[g] + lane] : 0;
+#pragma unroll
+            for (int g = 0; g < GG; g++) {
+                if (j[g] < 0) break;
+                const uint64_t mb = __ballot((uint32_t)lane < c[g] && rec_match(rec[g], v[g]));
+                uint32_t r;
+                if (mb) r = readlane((uint32_t)(rec[g] >> 32), __builtin_ctzll(mb));
+                else r = c[g] > 64 ? scan_tail(rules, o[g], c[g], v[g], 64, lane) : 0;
+                if (lane == j[g]) result = r;
+            }
         }
 
         // ---- verdict (kernel.c:444-456) and statistics (kernel.c:376-387)
         const uint32_t action = result & 0xFFu;
         const uint32_t key = (result >> 8) & 0xFFFFu;
         if (valid) {
-            if (kResults) results[i] = result;
-            if (kVerdicts)
-                verdicts[i] = (pk == INFW_PK_DROP_SHORT || action == INFW_XDP_DROP) ? INFW_XDP_DROP
-                                                                                    : INFW_XDP_PASS;
-            if ((action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys) {
+            if (results) {
+                if (!(kAblate & 16)) __builtin_nontemporal_store(result, &results[i]);
+                else results[i] = result;
+            }
+            if (verdicts)
+                verdicts[i] = (pk == INFW_PK_DROP_SHORT || action == INFW_XDP_DROP) ? INFW_XDP_DROP : INFW_XDP_PASS;
+            if (!(kAblate & 4) && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys) {
                 const int s = (int)key * 2 + (action == INFW_XDP_DROP);
                 atomicAdd(&s_pk[s], 1u);
                 atomicAdd(&s_by[s], (unsigned long long)plen);
@@ -123,23 +227,54 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const infw_dev_tables 
     }
 }
 
+template <int kBlock, int G, int kAblate = 0>
+void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
+            uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
+    const uint64_t tiles = (n + kBlock - 1) / kBlock;
+    const uint64_t grid = (uint64_t)grid_per_cu * cus;
+    const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results,
+                       verdicts, st);
+}
+
 }  // namespace
 
-// Host-side launcher (called from abi.cpp).  grid: persistent workgroup count.
+// Host-side launcher (called from abi.cpp).
+//   block: 256 or 512 threads; group: 0 = decision tables (default), else the
+//   one-lane-per-rule ballot scan with that many packets in flight (1, 4, 8);
+//   blocks_per_cu: resident workgroups per CU (LDS: 24 KiB each).
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
-                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats,
-                                    uint32_t grid, hipStream_t stream) {
+                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
+                                    int block, int group, int blocks_per_cu, hipStream_t stream) {
     if (n == 0) return 0;
-    uint64_t tiles = (n + kBlock - 1) / kBlock;
-    uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
     auto *st = reinterpret_cast<unsigned long long *>(stats);
-    if (results && verdicts)
-        hipLaunchKernelGGL((classify_kernel<true, true>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results, verdicts, st);
-    else if (results)
-        hipLaunchKernelGGL((classify_kernel<true, false>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results, verdicts, st);
-    else if (verdicts)
-        hipLaunchKernelGGL((classify_kernel<false, true>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results, verdicts, st);
-    else
-        hipLaunchKernelGGL((classify_kernel<false, false>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results, verdicts, st);
+    const uint32_t bpc = (uint32_t)blocks_per_cu;
+    if (const char *e = getenv("INFW_ABLATE")) {  // diagnostic builds of the 512/8 shape; results are not valid
+        switch (atoi(e)) {
+        case 0: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 32: launch<512, 8, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 1: launch<512, 0, 1>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 2: launch<512, 0, 2>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 4: launch<512, 0, 4>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 8: launch<512, 0, 8>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 3: launch<512, 0, 3>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (group == 0) {
+        if (block == 256) launch<256, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else launch<512, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    } else if (block == 256) {
+        if (group == 1) launch<256, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else if (group == 4) launch<256, 4>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else launch<256, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    } else {
+        if (group == 1) launch<512, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else if (group == 4) launch<512, 4>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else launch<512, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -70,9 +70,13 @@ struct HostTables {
     std::vector<uint32_t> tbl24;  // n_slots << 24
     std::vector<uint32_t> tbl8;
     std::vector<infw_long_entry> ltab;
+    std::vector<infw_v6_bucket> btab;
+    uint64_t n_buckets = 0, n_overflow_groups = 0;
     std::vector<uint8_t> levels;
     std::vector<uint64_t> desc;
     std::vector<uint64_t> rules;
+    std::vector<uint64_t> ddesc;
+    std::vector<uint32_t> dt;
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -82,7 +86,11 @@ struct HostTables {
 
 int compile_tables(const PendingMap &m, HostTables &out);
 
-// Class-filtered GPU rule records of one 1200-B value (appended to rules).
-void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE]);
+// Class-filtered GPU rule records of one 1200-B value (appended to rules) and
+// the per-class first-match decision tables (appended to dt).
+void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE],
+                       std::vector<uint32_t> &dt, uint64_t ddesc_out[INFW_DESC_STRIDE]);
+// Decision table of one class list (records {lo16, hi16, result32} in scan order).
+uint64_t build_decision_table(const std::vector<uint64_t> &recs, std::vector<uint32_t> &dt);
 
 }  // namespace infw

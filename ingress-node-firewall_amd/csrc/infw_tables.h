@@ -57,6 +57,35 @@ struct infw_long_entry {    // 32 B
     uint32_t pad[2];
 };
 
+// IPv6 long prefixes grouped by (slot, address bits 0..31): one 64-B bucket
+// holds up to 3 records of the group sorted longest first, so the first match
+// is the longest; a larger group sets n = INFW_BUCKET_OVERFLOW and is looked
+// up in the Waldvogel table instead.
+#define INFW_BUCKET_INLINE 3
+#define INFW_BUCKET_OVERFLOW 0xFFu
+struct infw_v6_rec {        // 16 B
+    uint64_t lo;            // address bits 64..127 (masked)
+    uint32_t mid;           // address bits 32..63 (masked)
+    uint32_t meta;          // (length - 32) << 25 | list+1
+};
+struct infw_v6_bucket {     // 64 B
+    uint32_t tag;           // slot + 1, 0 = empty
+    uint32_t top;           // address bits 0..31
+    uint32_t n;             // records, or INFW_BUCKET_OVERFLOW
+    uint32_t pad;
+    struct infw_v6_rec rec[INFW_BUCKET_INLINE];
+};
+
+// First-match decision tables.  For one (rule list, packet class) the
+// first-match result as a function of the 16-bit packet value (dport, or
+// type << 8 | code) is a step function with S <= 2c + 1 segments.  It is stored
+// as a static 9-ary search tree over the segment starts (8 u16 keys per 16-B
+// node, key = start - 1 so that "key < v" <=> "start <= v"; pad 0xFFFF never
+// counts) followed by the S result words.  ddesc[list*8 + cls]:
+//   S == 0: no applicable rule (result 0); S == 1: bits 0..31 = the result;
+//   else bits 0..31 = offset in 16-B units, 32..47 = S, 48..55 = depth d.
+#define INFW_DT_FANOUT 9
+
 struct infw_dev_tables {
     const uint32_t *if_keys;
     const uint32_t *if_slot;   // INFW_IF_EMPTY = free
@@ -66,10 +95,14 @@ struct infw_dev_tables {
     const uint32_t *tbl8;
     const struct infw_long_entry *ltab;
     uint64_t lmask;
-    const uint64_t *desc;
+    const struct infw_v6_bucket *btab;
+    uint64_t bmask;
+    const uint64_t *desc;      // ballot mode: off | cnt << 32 into rules
     const uint64_t *rules;
+    const uint64_t *ddesc;     // decision mode (see above)
+    const uint32_t *dt;          // decision-table pool, 16-B units
+    const uint8_t *levels;     // n_levels distinct long lengths, ascending
     uint32_t n_levels;
-    uint8_t levels[INFW_MAX_LEVELS];
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -80,6 +113,24 @@ INFW_TD uint64_t infw_be64(uint32_t w0, uint32_t w1) {  // bytes w0[0..3] w1[0..
 }
 
 INFW_TD uint32_t infw_if_hash(uint32_t ifindex) { return ifindex * 0x9E3779B1u; }
+
+INFW_TD uint64_t infw_bucket_hash(uint32_t slot, uint32_t top) {
+    uint64_t h = ((uint64_t)slot << 32 | top) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 30);
+}
+
+// Does record r cover address bits 32..127 (mid, lo)?
+INFW_TD bool infw_rec_match(uint32_t rmid, uint64_t rlo, uint32_t meta, uint32_t mid, uint64_t lo) {
+    const uint32_t L = (meta >> 25) + 32;  // 33..128
+    if (L <= 64) {
+        const uint32_t m = ~0u << (64 - L);  // L-32 in 1..32 leading bits of mid
+        return ((mid ^ rmid) & m) == 0;
+    }
+    const uint64_t m = L >= 128 ? ~0ull : ~0ull << (128 - L);
+    return mid == rmid && ((lo ^ rlo) & m) == 0;
+}
 
 INFW_TD uint64_t infw_long_hash(uint32_t tag, uint64_t hi, uint64_t lo) {
     uint64_t h = hi * 0x9E3779B97F4A7C15ull;
@@ -127,6 +178,29 @@ INFW_TD int infw_parse(uint32_t meta, uint32_t l4word, int *cls, uint32_t *val) 
     else *val = (l4word << 8 & 0xFF00u) | (l4word >> 8 & 0xFFu);              // type << 8 | code
     *cls = c;
     return v4 ? INFW_PK_V4 : INFW_PK_V6;
+}
+
+INFW_TD uint32_t infw_count_lt(uint32_t w, uint32_t v) {  // keys (two u16) below v
+    return (uint32_t)((w & 0xFFFFu) < v) + (uint32_t)((w >> 16) < v);
+}
+
+// First-match result of decision-table descriptor dd for value v.
+template <class T>
+INFW_TD uint32_t infw_dt_eval(const T &t, uint64_t dd, uint32_t v) {
+    const uint32_t S = (uint32_t)(dd >> 32) & 0xFFFFu;
+    if (S <= 1) return S ? (uint32_t)dd : 0u;
+    const uint32_t d = (uint32_t)(dd >> 48) & 0xFFu;
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(t.dt) + 4ull * (uint32_t)dd;
+    uint32_t node = 0, lvl = 0, span = d == 1 ? 9u : d == 2 ? 81u : 729u;
+    for (uint32_t l = 0; l < d; l++) {
+        const uint32_t *k = base + 4ull * (lvl + node);
+        const uint32_t c = infw_count_lt(k[0], v) + infw_count_lt(k[1], v) + infw_count_lt(k[2], v) +
+                           infw_count_lt(k[3], v);
+        lvl += (S + span - 1) / span;  // nodes on level l
+        span /= 9u;
+        node = node * 9u + c;
+    }
+    return base[4ull * lvl + node];
 }
 
 // Table pointers are read through T so host and device share the walk.
@@ -177,6 +251,30 @@ INFW_TD uint32_t infw_long_lookup(const T &t, uint32_t slot, uint64_t hi, uint64
     return best;
 }
 
+// Longest long (/33../128) prefix covering an IPv6 address: its /32 group's
+// bucket, or the Waldvogel table when the group overflowed.  list+1 or 0.
+template <class T>
+INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uint32_t sa[4]) {
+    const uint32_t mid = infw_bswap32(sa[1]);
+    const uint64_t lo = infw_be64(sa[2], sa[3]);
+    uint64_t i = infw_bucket_hash(slot, a32) & t.bmask;
+    for (;;) {
+        const struct infw_v6_bucket *b = &t.btab[i];
+        const uint32_t tag = b->tag;
+        if (tag == 0) return 0;
+        if (tag == slot + 1 && b->top == a32) {
+            const uint32_t nb = b->n;
+            if (nb == INFW_BUCKET_OVERFLOW) return infw_long_lookup(t, slot, (uint64_t)a32 << 32 | mid, lo);
+            for (uint32_t k = 0; k < nb; k++) {
+                const struct infw_v6_rec r = b->rec[k];
+                if (infw_rec_match(r.mid, r.lo, r.meta, mid, lo)) return r.meta & 0x1FFFFFFu;
+            }
+            return 0;
+        }
+        i = (i + 1) & t.bmask;
+    }
+}
+
 // list+1 of the longest matching entry, 0 if none.
 template <class T>
 INFW_TD uint32_t infw_lpm(const T &t, int pk, uint32_t ifindex, const uint32_t sa[4]) {
@@ -184,7 +282,7 @@ INFW_TD uint32_t infw_lpm(const T &t, int pk, uint32_t ifindex, const uint32_t s
     if (slot < 0) return 0;
     uint32_t a32 = infw_bswap32(sa[0]);
     if (pk == INFW_PK_V6 && t.n_levels) {
-        uint32_t r = infw_long_lookup(t, (uint32_t)slot, infw_be64(sa[0], sa[1]), infw_be64(sa[2], sa[3]));
+        uint32_t r = infw_v6_long(t, (uint32_t)slot, a32, sa);
         if (r) return r;
     }
     return infw_dir_lookup(t, (uint32_t)slot, a32);

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <numeric>
+#include <queue>
 
 #include "infw_internal.h"
 
@@ -183,8 +184,77 @@ int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
 //   any other protocol               can never match: dropped
 // result32 = SET_ACTIONRULE_RESPONSE(action, ruleId) (ingress_node_firewall.h:22).
 // ------------------------------------------------------------------------
+// First-match step function of a class list: sweep the 16-bit value axis
+// keeping the lowest-index rule covering it (min-heap with lazy deletion),
+// merge equal neighbours, then lay the segment starts out as a 9-ary search
+// tree (infw_tables.h) followed by the results.
+uint64_t build_decision_table(const std::vector<uint64_t> &recs, std::vector<uint32_t> &dt) {
+    const size_t c = recs.size();
+    if (c == 0) return 0;
+    std::vector<std::pair<uint32_t, uint32_t>> ev;  // (position, rule index) starts
+    std::vector<std::pair<uint32_t, uint32_t>> en;  // (position, rule index) ends (hi + 1)
+    std::vector<uint32_t> pts{0};
+    for (uint32_t i = 0; i < c; i++) {
+        uint32_t lo = (uint32_t)recs[i] & 0xFFFFu, hi = (uint32_t)(recs[i] >> 16) & 0xFFFFu;
+        ev.emplace_back(lo, i);
+        pts.push_back(lo);
+        if (hi + 1 <= 0xFFFFu) {
+            en.emplace_back(hi + 1, i);
+            pts.push_back(hi + 1);
+        }
+    }
+    std::sort(pts.begin(), pts.end());
+    pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+    std::sort(ev.begin(), ev.end());
+    std::sort(en.begin(), en.end());
+    std::vector<uint8_t> active(c, 0);
+    std::priority_queue<uint32_t, std::vector<uint32_t>, std::greater<uint32_t>> heap;
+    std::vector<uint32_t> starts, res;
+    size_t ie = 0, in = 0;
+    for (uint32_t p : pts) {
+        while (in < en.size() && en[in].first == p) active[en[in++].second] = 0;
+        while (ie < ev.size() && ev[ie].first == p) {
+            active[ev[ie].second] = 1;
+            heap.push(ev[ie++].second);
+        }
+        while (!heap.empty() && !active[heap.top()]) heap.pop();
+        uint32_t r = heap.empty() ? 0u : (uint32_t)(recs[heap.top()] >> 32);
+        if (res.empty() || res.back() != r) {
+            starts.push_back(p);
+            res.push_back(r);
+        }
+    }
+    const uint32_t S = (uint32_t)starts.size();
+    if (S == 1) return (uint64_t)res[0] | 1ull << 32;
+    uint32_t d = 1, span = 9;
+    while (span < S) {
+        d++;
+        span *= 9;
+    }
+    // offset in 16-B units
+    while (dt.size() & 3) dt.push_back(0);
+    const uint64_t off = dt.size() / 4;
+    if (off > 0xFFFFFFFFull) return ~0ull;
+    uint32_t sp = span;
+    for (uint32_t l = 0; l < d; l++) {
+        const uint32_t nodes = (S + sp - 1) / sp, child = sp / 9;
+        for (uint32_t k = 0; k < nodes; k++) {
+            uint16_t key[8];
+            for (uint32_t j = 0; j < 8; j++) {
+                uint64_t seg = ((uint64_t)k * 9 + j + 1) * child;
+                key[j] = seg < S ? (uint16_t)(starts[seg] - 1) : (uint16_t)0xFFFF;
+            }
+            for (uint32_t w = 0; w < 4; w++) dt.push_back((uint32_t)key[2 * w] | (uint32_t)key[2 * w + 1] << 16);
+        }
+        sp = child;
+    }
+    dt.insert(dt.end(), res.begin(), res.end());
+    return off | (uint64_t)S << 32 | (uint64_t)d << 48;
+}
+
 void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
-                       uint64_t desc_out[INFW_DESC_STRIDE]) {
+                       uint64_t desc_out[INFW_DESC_STRIDE], std::vector<uint32_t> &dt,
+                       uint64_t ddesc_out[INFW_DESC_STRIDE]) {
     std::vector<uint64_t> per[INFW_NCLS];
     for (int i = 0; i < INFW_MAX_RULES_PER_TARGET; i++) {
         const uint8_t *r = val + 12 * i;
@@ -222,6 +292,7 @@ void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
         }
     }
     for (int c = 0; c < INFW_DESC_STRIDE; c++) {
+        ddesc_out[c] = c < INFW_NCLS ? build_decision_table(per[c], dt) : 0;
         if (c >= INFW_NCLS || per[c].empty()) {
             desc_out[c] = 0;
             continue;
@@ -322,6 +393,7 @@ int compile_tables(const PendingMap &m, HostTables &out) {
     }
     out.n_lists = (uint32_t)list_of_vid.size();
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
+    out.ddesc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
     {
         std::vector<std::pair<uint32_t, uint32_t>> by_lid(list_of_vid.begin(), list_of_vid.end());
         std::sort(by_lid.begin(), by_lid.end(),
@@ -329,9 +401,16 @@ int compile_tables(const PendingMap &m, HostTables &out) {
                       return a.second < b.second;
                   });
         for (auto &p : by_lid)
-            compile_rule_list(m.pool.vals[p.first].data(), out.rules, &out.desc[(size_t)p.second * INFW_DESC_STRIDE]);
+            compile_rule_list(m.pool.vals[p.first].data(), out.rules, &out.desc[(size_t)p.second * INFW_DESC_STRIDE],
+                              out.dt, &out.ddesc[(size_t)p.second * INFW_DESC_STRIDE]);
     }
+    for (uint64_t dd : out.ddesc)
+        if (dd == ~0ull) {
+            set_error("compile: decision-table pool exceeds 64 GiB");
+            return -ENOSPC;
+        }
     if (out.rules.empty()) out.rules.push_back(0);
+    while (out.dt.size() < 4 || (out.dt.size() & 3)) out.dt.push_back(0);
 
     // --- split entries
     std::vector<ShortEnt> shorts;
@@ -455,6 +534,50 @@ int compile_tables(const PendingMap &m, HostTables &out) {
         }
         out.n_long_entries = set.n;
     }
+
+    // --- /32-grouped buckets for IPv6 long prefixes (the fast path)
+    {
+        struct G {
+            uint32_t slot, top;
+            std::vector<infw_v6_rec> recs;
+        };
+        std::unordered_map<uint64_t, G> groups;
+        for (const auto &r : longs) {
+            uint32_t top = (uint32_t)(r.hi >> 32);
+            G &g = groups[(uint64_t)r.slot << 32 | top];
+            g.slot = r.slot;
+            g.top = top;
+            if (r.list1 >= (1u << 25)) {
+                set_error("compile: more than 2^25-1 rule lists");
+                return -ENOSPC;
+            }
+            g.recs.push_back(infw_v6_rec{r.lo, (uint32_t)r.hi, (r.len - 32) << 25 | r.list1});
+        }
+        uint64_t cap = 1024;
+        while (cap < groups.size() * 2) cap <<= 1;
+        out.btab.assign(cap, infw_v6_bucket{});
+        memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
+        const uint64_t bmask = cap - 1;
+        for (auto &kv : groups) {
+            G &g = kv.second;
+            uint64_t i = infw_bucket_hash(g.slot, g.top) & bmask;
+            while (out.btab[i].tag) i = (i + 1) & bmask;
+            infw_v6_bucket &b = out.btab[i];
+            b.tag = g.slot + 1;
+            b.top = g.top;
+            if (g.recs.size() > INFW_BUCKET_INLINE) {
+                b.n = INFW_BUCKET_OVERFLOW;
+                out.n_overflow_groups++;
+            } else {
+                // longest first: the first covering record is the longest match
+                std::sort(g.recs.begin(), g.recs.end(),
+                          [](const infw_v6_rec &a, const infw_v6_rec &c) { return a.meta > c.meta; });
+                b.n = (uint32_t)g.recs.size();
+                for (size_t k = 0; k < g.recs.size(); k++) b.rec[k] = g.recs[k];
+            }
+        }
+        out.n_buckets = groups.size();
+    }
     return 0;
 }
 
@@ -469,10 +592,14 @@ infw_dev_tables HostTables::view() const {
     t.tbl8 = tbl8.data();
     t.ltab = ltab.data();
     t.lmask = ltab.size() - 1;
+    t.btab = btab.data();
+    t.bmask = btab.size() - 1;
     t.desc = desc.data();
     t.rules = rules.data();
+    t.ddesc = ddesc.data();
+    t.dt = dt.data();
     t.n_levels = (uint32_t)levels.size();
-    for (size_t i = 0; i < levels.size(); i++) t.levels[i] = levels[i];
+    t.levels = levels.data();
     return t;
 }
 

@@ -77,7 +77,8 @@ class TableInfo(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("n_entries", C.c_uint64), ("n_if_slots", C.c_uint32),
                 ("n_lists", C.c_uint32), ("n_rules", C.c_uint64), ("n_tbl8_groups", C.c_uint64),
                 ("n_long_levels", C.c_uint32), ("n_long_entries", C.c_uint64),
-                ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double)]
+                ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double),
+                ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12
@@ -89,7 +90,7 @@ ABI_SYMBOLS = [
     "infw_table_delete", "infw_table_get_next_key", "infw_table_lookup", "infw_table_count",
     "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
-    "infw_table_info", "infw_debug_walk", "infw_last_error", "infw_abi_version",
+    "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
 ]
 
 
@@ -135,6 +136,7 @@ _sig = {
                                  C.c_char_p]),
     "infw_table_info": (C.c_int, [C.c_void_p, P(TableInfo)]),
     "infw_debug_walk": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "infw_set_launch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "infw_last_error": (C.c_char_p, []),
     "infw_abi_version": (C.c_int, []),
 }

@@ -155,6 +155,10 @@ class Classifier:
                            results.data_ptr() if results is not None else 0,
                            verdicts.data_ptr() if verdicts is not None else 0, sp)
 
+    def set_launch(self, block: int = 512, scan_group: int = 0, blocks_per_cu: int = 4) -> None:
+        """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
+        check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")
+
     # -- statistics map
     def stats_read(self, rule_id: int) -> List[RuleStatisticsSt]:
         """Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt): one entry per device slot."""

@@ -1,0 +1,135 @@
+"""Table compiler (host side of the GPU tables) against the oracle, on the CPU.
+
+The product compiles the table map into DIR-24-8 + IPv6 /32 buckets +
+Waldvogel overflow table + class-filtered rule lists; infw_debug_walk runs the
+kernel's lookup code over that image on the host.  These tests compare it with
+the oracle on the BASELINE workloads and on adversarial random tables.
+"""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import infw
+import orc
+from infw import workloads as W
+
+
+def walk_vs_oracle(entries, tuples_from, n=20000, seed=1):
+    """entries: list of (key bytes, value bytes)."""
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    m = orc.OracleMap()
+    for k, v in entries:
+        rc = c.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v))
+        assert rc == m.update(k, v)
+    c.commit()
+    hdr, cap, pl, ifx = tuples_from(n, seed)
+    res, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=4)
+    got = c.debug_walk(W.pack_frames(hdr, cap, pl, ifx))
+    bad = np.nonzero(got != res)[0]
+    assert bad.size == 0, (bad[:5], got[bad[:5]], res[bad[:5]])
+    return c, res
+
+
+@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG0_DEMO, 0, 0), (W.CFG1_V4_10K, 0, 0),
+                                            (W.CFG2_MIXED_1M, 100000, 512), (W.CFG4_ADVERSARIAL, 20000, 64)])
+def test_workloads(cfg, npfx, ntmpl):
+    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
+    walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
+
+
+def _val(rng, rid_base):
+    import goenc
+    rules = []
+    for slot in rng.sample(range(1, 100), 6):
+        proto = rng.choice([0, 6, 17, 132, 1, 58, 47])
+        ps = rng.randrange(0, 65536)
+        pe = rng.choice([0, 0, min(65535, ps + rng.randrange(0, 300)), rng.randrange(0, 65536)])
+        rules.append({"slot": slot, "ruleId": rng.choice([slot, slot + rid_base, 0, 1024, 65536 + slot]),
+                      "protocol": proto, "dstPortStart": ps, "dstPortEnd": pe, "icmpType": rng.randrange(256),
+                      "icmpCode": rng.randrange(4), "action": rng.choice([1, 2, 2, 1, 0, 3])})
+    return goenc.raw_value(rules)
+
+
+def _clustered_table(rng, n_groups=40):
+    """IPv6 prefixes clustered under few /32s (overflow groups), nested lengths 0..128 on 3 ifindexes,
+    cross-family aliases, plus IPv4 nesting — every LPM corner the layout has."""
+    ents = []
+    anchors = []
+    for g in range(n_groups):
+        ifx = rng.choice([3, 4, 70000])
+        top = rng.getrandbits(32)
+        anchors.append((ifx, top))
+        for _ in range(rng.choice([1, 2, 3, 4, 9, 25])):   # > 3 -> overflow group
+            L = rng.choice([33, 40, 47, 48, 56, 63, 64, 65, 96, 127, 128])
+            addr = (top << 96) | rng.getrandbits(96)
+            ents.append((ifx, L + 32, addr.to_bytes(16, "big")))
+        for L in (0, 8, 16, 24, 30, 32):                     # short prefixes over the same bits (v6-written)
+            ents.append((ifx, L + 32, ((top << 96) | rng.getrandbits(96)).to_bytes(16, "big")))
+    for _ in range(300):                                      # IPv4 nesting
+        ifx = rng.choice([3, 4])
+        a = rng.getrandbits(32) & 0xFFFFFF00 if rng.random() < 0.5 else rng.getrandbits(32)
+        for L in (8, 16, 20, 24, 25, 28, 32):
+            if rng.random() < 0.4:
+                ents.append((ifx, L + 32, a.to_bytes(4, "big") + b"\0" * 12))
+    out = []
+    for i, (ifx, plen, ip) in enumerate(ents):
+        out.append((struct.pack("<II", plen, ifx) + ip, _val(rng, i)))
+    return out, anchors
+
+
+def test_clustered_overflow_groups():
+    rng = random.Random(7)
+    entries, anchors = _clustered_table(rng)
+    from frames import frame, snapshots
+
+    def packets(n, seed):
+        r = random.Random(seed)
+        fr, ifx = [], []
+        for _ in range(n):
+            i, top = r.choice(anchors)
+            if r.random() < 0.15:
+                i = r.choice([3, 4, 5, 70000])
+            if r.random() < 0.7:
+                a = (top << 96) | r.getrandbits(96)
+                src = str(__import__("ipaddress").IPv6Address(a))
+            elif r.random() < 0.5:
+                src = str(__import__("ipaddress").IPv4Address(top))
+            else:
+                src = str(__import__("ipaddress").IPv4Address(r.getrandbits(32)))
+            proto = r.choice(["tcp", "udp", "sctp", "icmp", "icmpv6", 1, 58, "gre"])
+            fr.append(frame(src, proto=proto, dport=r.randrange(65536), icmp_type=r.randrange(256),
+                            icmp_code=r.randrange(4), length=r.randrange(60, 1500)))
+            ifx.append(i)
+        hdr, cap, pl = snapshots(fr)
+        return hdr, cap, pl, np.array(ifx, np.uint32)
+
+    c, res = walk_vs_oracle(entries, packets, n=6000)
+    info = c.info()
+    assert info["n_v6_overflow"] > 0 and info["n_v6_groups"] > info["n_v6_overflow"]
+    assert (res != 0).mean() > 0.3
+
+
+def test_update_delete_churn_matches_oracle():
+    """Random update/delete/commit churn: the compiled image tracks the map exactly."""
+    rng = random.Random(11)
+    entries, anchors = _clustered_table(rng, n_groups=15)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    m = orc.OracleMap()
+    from frames import frame, snapshots
+    fr = [frame(str(__import__("ipaddress").IPv6Address((t << 96) | rng.getrandbits(96))), proto="udp",
+                dport=rng.randrange(65536)) for _, t in anchors for _ in range(20)]
+    ifx = np.array([i for i, _ in anchors for _ in range(20)], np.uint32)
+    hdr, cap, pl = snapshots(fr)
+    tup = W.pack_frames(hdr, cap, pl, ifx)
+    for step in range(6):
+        for k, v in rng.sample(entries, len(entries) // 3):
+            if rng.random() < 0.4:
+                assert c.delete_rc(infw.LpmIpKeySt.from_buffer_copy(k)) == m.delete(k)
+            else:
+                assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == \
+                    m.update(k, v)
+        c.commit()
+        res, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
+        assert np.array_equal(c.debug_walk(tup), res), step
