@@ -1,0 +1,63 @@
+"""Multi-process path on the CPU (gloo, world size 2): each rank classifies its own
+contiguous shard of the global packet index range and the per-rule counters are
+all-reduced — the same sharding and exchange bench.py does over RCCL — and the
+totals equal a single-process run over the whole range.
+
+The per-rank classification here is the product's compiled-table walk on the host
+(infw_debug_walk); on the GPU box the HIP kernel does it (tests/test_gpu_parity.py)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N_TOTAL = 1 << 16
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stats_for(start, n):
+    import infw
+    from infw import workloads as W
+    from parity import stats_from_results
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    wl.load_into(c)
+    c.commit()
+    t = wl.tuples(start, n)
+    return stats_from_results(c.debug_walk(t), t[:, 5])
+
+
+def _worker(rank, world, port, out_path):
+    sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)),
+                    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ingress-node-firewall_amd"),
+                    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = N_TOTAL // world
+    st = torch.from_numpy(_stats_for(rank * n, n).view(np.int64).copy())
+    dist.all_reduce(st)                       # bench.py: dist.all_reduce(stats) over RCCL
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py: max-over-ranks timing
+    if rank == 0:
+        np.save(out_path, st.numpy().view(np.uint64))
+        assert t.item() == world
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_allreduce_equal_single_process(tmp_path):
+    out = str(tmp_path / "st.npy")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    got = np.load(out)
+    want = _stats_for(0, N_TOTAL)
+    assert np.array_equal(got, want)
+    assert got[:, 0].sum() + got[:, 2].sum() > N_TOTAL // 2

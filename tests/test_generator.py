@@ -1,0 +1,35 @@
+"""Synthetic workload generator: packet i is a pure function of (seed, i); the host
+frame builder + packer and the tuple generator agree; shards are independent of
+the shard split (what makes the multi-GPU totals GPU-count invariant)."""
+import numpy as np
+
+from infw import workloads as W
+
+
+def test_pack_equals_generated_tuples_all_configs():
+    for cfg, kw in ((W.CFG0_DEMO, {}), (W.CFG1_V4_10K, {}), (W.CFG2_MIXED_1M, dict(n_prefixes=20000, n_templates=64)),
+                    (W.CFG4_ADVERSARIAL, dict(n_prefixes=5000, n_templates=16))):
+        wl = W.Workload(cfg, **kw)
+        hdr, cap, pl, ifx = wl.frames(12345, 50000)
+        assert np.array_equal(W.pack_frames(hdr, cap, pl, ifx), wl.tuples(12345, 50000)), cfg
+
+
+def test_shard_invariance():
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    whole = wl.tuples(0, 40000)
+    parts = np.concatenate([wl.tuples(a, 10000) for a in (0, 10000, 20000, 30000)])
+    assert np.array_equal(whole, parts)
+    wl2 = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    assert np.array_equal(wl2.tuples(777, 1000), whole[777:1777])
+
+
+def test_workload_mix_is_as_specified():
+    wl = W.Workload(W.CFG0_DEMO)
+    t = wl.tuples(0, 200000)
+    et = t[:, 6] & 0xFFFF
+    v4, v6 = (et == 0x0800).mean(), (et == 0x86DD).mean()
+    assert 0.45 < v4 < 0.55 and 0.45 < v6 < 0.55
+    proto = (t[:, 6] >> 16) & 0xFF
+    assert 0.55 < (proto == 6).mean() < 0.65
+    assert ((t[:, 6] >> 24) < 54).mean() > 0.001        # some truncated frames
+    assert (t[:, 5] >= 54).mean() > 0.99                  # frame lengths U[54, 1514]
