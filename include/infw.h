@@ -202,6 +202,35 @@ int infw_classify(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint6
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
 
 /* ------------------------------------------------------------------------ */
+/* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */
+/*  - Deny events (kernel.c:392-399, ingress_node_firewall_events_map): one  */
+/*    record per DROP-by-rule packet: the 8-B event_hdr_st the program       */
+/*    emits plus where the min(len, 256) packet bytes of the perf record     */
+/*    live (the batch index).  Records are appended with one atomic per      */
+/*    wave; order across waves is unspecified, like perf records across      */
+/*    CPUs; *events_count counts every event, also those beyond events_cap   */
+/*    (perf "lost samples").                                                  */
+/* ------------------------------------------------------------------------ */
+struct infw_event_rec {
+    struct event_hdr_st hdr;      /* ifId, ruleId, action (1), pad, pktLength (u16 truncations) */
+    uint32_t captured;            /* min(pkt_len, INFW_MAX_EVENT_DATA)                          */
+    uint32_t reserved;
+    uint64_t pkt_index;           /* batch index of the packet the record belongs to             */
+};
+
+struct infw_classify_ex {
+    uint32_t size;                /* sizeof(struct infw_classify_ex)                              */
+    uint32_t flags;               /* reserved, 0                                                 */
+    struct infw_event_rec *events;   /* device buffer, or NULL: no event stream                  */
+    uint64_t events_cap;
+    uint64_t *events_count;       /* device u64, incremented by the kernel                       */
+};
+
+int infw_classify_ex(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
+                     uint32_t *result_words, uint8_t *xdp_verdicts,
+                     const struct infw_classify_ex *ex, void *stream);
+
+/* ------------------------------------------------------------------------ */
 /* Statistics — ingress_node_firewall_statistics_map (kernel.c:36-41,        */
 /* PERCPU_ARRAY[1024] of ruleStatistics_st).  One slot per device plays the  */
 /* role of one per-CPU slot; readers sum slots like statistics.go:126-157.   */

@@ -13,7 +13,8 @@
 
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                    int block, int group, int blocks_per_cu, hipStream_t stream);
+                                    int block, int group, int blocks_per_cu, hipStream_t stream,
+                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count);
 
 namespace infw {
 
@@ -106,7 +107,9 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
     memset(&t, 0, sizeof(t));
     int rc = 0;
     if ((rc = upload(*ep, h.if_keys, &t.if_keys)) || (rc = upload(*ep, h.if_slot, &t.if_slot)) ||
-        (rc = upload(*ep, h.tbl24, &t.tbl24)) || (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
+        (rc = upload(*ep, h.l16, &t.l16)) || (rc = upload(*ep, h.nodes, &t.nodes)) ||
+        (rc = upload(*ep, h.vpool, &t.vpool)) || (rc = upload(*ep, h.tbl24, &t.tbl24)) ||
+        (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
         (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.btab, &t.btab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
         (rc = upload(*ep, h.rules, &t.rules)) ||
         (rc = upload(*ep, h.ddesc, &t.ddesc)) || (rc = upload(*ep, h.dt, &t.dt)) || (rc = upload(*ep, h.levels, &t.levels)))
@@ -273,7 +276,7 @@ int infw_table_commit(infw_ctx *ctx) {
     in.n_if_slots = h.n_slots;
     in.n_lists = h.n_lists;
     in.n_rules = h.rules.size();
-    in.n_tbl8_groups = h.tbl8.size() / 256;
+    in.n_tbl8_groups = h.n_tbl8_groups;
     in.n_long_levels = (uint32_t)h.levels.size();
     in.n_long_entries = h.n_long_entries;
     in.device_bytes = eps.empty() ? 0 : eps[0]->bytes;
@@ -324,6 +327,16 @@ int infw_table_info(infw_ctx *ctx, struct infw_table_info *info) {
 
 int infw_classify(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n,
                   uint32_t *result_words, uint8_t *xdp_verdicts, void *stream) {
+    return infw_classify_ex(ctx, dev, in, n, result_words, xdp_verdicts, nullptr, stream);
+}
+
+int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n, uint32_t *result_words,
+                     uint8_t *xdp_verdicts, const struct infw_classify_ex *ex, void *stream) {
+    if (ex && (ex->size < sizeof(struct infw_classify_ex) || ex->flags != 0 || (ex->events_cap && !ex->events) ||
+               (ex->events && !ex->events_count))) {
+        set_error("classify_ex: bad options");
+        return -EINVAL;
+    }
     if (!ctx || !in) return -EINVAL;
     if (ctx->devs.empty()) {
         set_error("classify: host-only context has no device tables");
@@ -349,8 +362,10 @@ int infw_classify(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n,
         set_error("hipSetDevice failed");
         return -ENODEV;
     }
+    const bool evs = ex && ex->events_count;
     int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.cus, ctx->block,
-                                  ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream));
+                                  ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream),
+                                  evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr);
     if (rc) {
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;

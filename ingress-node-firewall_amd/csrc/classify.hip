@@ -75,11 +75,18 @@ __device__ __forceinline__ uint32_t dt_eval(const uint32_t *__restrict__ dt, uin
 }
 
 // G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
-template <int kBlock, int G, int kAblate = 0>
+struct EventSink {
+    infw_event_rec *rec;
+    uint64_t cap;
+    unsigned long long *count;
+};
+
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false>
 __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
-                                                          unsigned long long *__restrict__ stats) {
+                                                          unsigned long long *__restrict__ stats,
+                                                          const EventSink ev) {
     __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
     __shared__ unsigned long long s_by[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
@@ -149,13 +156,18 @@ __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel
                 l1 = 0;
                 if (slot >= 0) {
                     const uint32_t a32 = infw_bswap32(sa.x);
-                    // the short-table word is fetched for every packet, alongside the
-                    // IPv6 bucket probe: IPv4 and IPv6 lanes issue their misses together
-                    const uint32_t e24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
-                    uint32_t lng = 0;
+                    // IPv6: the /32 group's bucket first; the short table only when no
+                    // long prefix covers the address (the kernel is bound by random
+                    // memory traffic, not latency: no speculative short-table fetch)
+                    uint32_t lng = 0, sh = 0;
+                    // A/B flags: 32 = DIR-24-8 image instead of the compressed table,
+                    // 64 = fetch the short table before (beside) the IPv6 bucket
+                    if (kAblate & 64) sh = (kAblate & 32) ? infw_dir24_lookup(T, (uint32_t)slot, a32)
+                                                          : infw_dir_lookup(T, (uint32_t)slot, a32);
                     if (pk == INFW_PK_V6 && T.n_levels) lng = infw_v6_long(T, (uint32_t)slot, a32, sw);
-                    l1 = lng;
-                    if (!lng) l1 = (e24 & INFW_TBL8_FLAG) ? T.tbl8[((uint64_t)(e24 & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu)] : e24;
+                    if (!(kAblate & 64) && !lng)
+                        sh = (kAblate & 32) ? infw_dir24_lookup(T, (uint32_t)slot, a32) : infw_dir_lookup(T, (uint32_t)slot, a32);
+                    l1 = lng ? lng : sh;
                 }
             }
             if (l1) d = (G == 0 ? T.ddesc : T.desc)[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
@@ -201,6 +213,25 @@ __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel
         // ---- verdict (kernel.c:444-456) and statistics (kernel.c:376-387)
         const uint32_t action = result & 0xFFu;
         const uint32_t key = (result >> 8) & 0xFFFFu;
+        if (kEvents) {  // deny events (kernel.c:392-399): one atomic per wave, lanes keep their order
+            const bool deny = valid && action == INFW_XDP_DROP;
+            const uint64_t m = __ballot(deny);
+            if (m) {
+                unsigned long long base = 0;
+                if (lane == __builtin_ctzll(m)) base = atomicAdd(ev.count, (unsigned long long)__popcll(m));
+                base = ((unsigned long long)readlane((uint32_t)(base >> 32), __builtin_ctzll(m)) << 32) |
+                       readlane((uint32_t)base, __builtin_ctzll(m));
+                const uint64_t slot = base + __popcll(m & ((1ull << lane) - 1));
+                if (deny && slot < ev.cap) {
+                    uint64_t *r = reinterpret_cast<uint64_t *>(ev.rec + slot);
+                    // event_hdr_st {ifId, ruleId, action, pad, pktLength}: u16 truncations (kernel.c:370-373)
+                    r[0] = (uint64_t)(ifx & 0xFFFFu) | (uint64_t)key << 16 | (uint64_t)INFW_XDP_DROP << 32 |
+                           (uint64_t)(plen & 0xFFFFu) << 48;
+                    r[1] = (uint64_t)(plen < INFW_MAX_EVENT_DATA ? plen : INFW_MAX_EVENT_DATA);
+                    r[2] = i;
+                }
+            }
+        }
         if (valid) {
             if (results) {
                 if (!(kAblate & 16)) __builtin_nontemporal_store(result, &results[i]);
@@ -227,14 +258,15 @@ __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel
     }
 }
 
-template <int kBlock, int G, int kAblate = 0>
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
-            uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
+            uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
+            EventSink ev = EventSink{nullptr, 0, nullptr}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n, results,
-                       verdicts, st);
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n,
+                       results, verdicts, st, ev);
 }
 
 }  // namespace
@@ -245,19 +277,30 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
 //   blocks_per_cu: resident workgroups per CU (LDS: 24 KiB each).
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                    int block, int group, int blocks_per_cu, hipStream_t stream) {
+                                    int block, int group, int blocks_per_cu, hipStream_t stream,
+                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count) {
     if (n == 0) return 0;
+    if (ev_count) {  // event stream: the default launch shape with the sideband compiled in
+        auto *stt = reinterpret_cast<unsigned long long *>(stats);
+        launch<512, 0, 0, true>((uint32_t)blocks_per_cu, cus, T, in, n, results, verdicts, stt, stream,
+                                EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)});
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
     const uint32_t bpc = (uint32_t)blocks_per_cu;
     if (const char *e = getenv("INFW_ABLATE")) {  // diagnostic builds of the 512/8 shape; results are not valid
         switch (atoi(e)) {
         case 0: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 32: launch<512, 8, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 1: launch<512, 0, 1>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 2: launch<512, 0, 2>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 4: launch<512, 0, 4>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 8: launch<512, 0, 8>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 3: launch<512, 0, 3>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 32: launch<512, 0, 32>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 96: launch<512, 0, 96>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 34: launch<512, 0, 34>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 98: launch<512, 0, 98>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;

@@ -67,8 +67,11 @@ void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes);
 struct HostTables {
     std::vector<uint32_t> if_keys, if_slot;
     uint32_t n_slots = 0;
-    std::vector<uint32_t> tbl24;  // n_slots << 24
-    std::vector<uint32_t> tbl8;
+    std::vector<uint32_t> l16;    // n_slots << 16
+    std::vector<infw_bnode> nodes;
+    std::vector<uint32_t> vpool;
+    uint64_t n_tbl8_groups = 0;   // DIR-24-8 second-level groups of the build image
+    std::vector<uint32_t> tbl24, tbl8;  // the DIR-24-8 image itself (kept for A/B)
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;
     uint64_t n_buckets = 0, n_overflow_groups = 0;

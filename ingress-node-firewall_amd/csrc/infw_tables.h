@@ -86,12 +86,31 @@ struct infw_v6_bucket {     // 64 B
 //   else bits 0..31 = offset in 16-B units, 32..47 = S, 48..55 = depth d.
 #define INFW_DT_FANOUT 9
 
+// Compressed short table (the <= /32 key space), per slot: l16[slot][2^16]
+// words indexed by address bits 0..15; a word is list+1 (0 = none) or, with
+// bit 31 set, the index of a 64-B node resolving the next 8 bits.  A node
+// keeps a 256-bit run bitmap (bit i set: child i differs from child i-1; bit 0
+// always set) and the run values, inline when there are at most 6, else in
+// vpool[base ..].  Child i's value is run popcount(bm[0..i]) - 1; values have
+// the same encoding (bits 24..31 via a second node level).
+#define INFW_NODE_FLAG 0x80000000u
+#define INFW_NODE_INLINE 6
+struct infw_bnode {         // 64 B
+    uint32_t bm[8];
+    uint32_t nv;            // runs
+    uint32_t base;          // vpool index when nv > INFW_NODE_INLINE
+    uint32_t v[INFW_NODE_INLINE];
+};
+
 struct infw_dev_tables {
     const uint32_t *if_keys;
     const uint32_t *if_slot;   // INFW_IF_EMPTY = free
     uint32_t if_mask;
     uint32_t n_slots;
-    const uint32_t *tbl24;
+    const uint32_t *l16;       // n_slots << 16
+    const struct infw_bnode *nodes;
+    const uint32_t *vpool;
+    const uint32_t *tbl24;     // DIR-24-8 image of the same short table (A/B), n_slots << 24
     const uint32_t *tbl8;
     const struct infw_long_entry *ltab;
     uint64_t lmask;
@@ -215,10 +234,43 @@ INFW_TD int infw_if_slot(const T &t, uint32_t ifindex) {
     }
 }
 
+INFW_TD uint32_t infw_popc(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__popc(x);
+#else
+    return (uint32_t)__builtin_popcount(x);
+#endif
+}
+
+// Value of child i (0..255) of node n.
 template <class T>
-INFW_TD uint32_t infw_dir_lookup(const T &t, uint32_t slot, uint32_t a32) {
+INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_t i) {
+    const uint32_t w = i >> 5, b = i & 31;
+    uint32_t r = infw_popc(n.bm[w] & (0xFFFFFFFFu >> (31 - b)));
+    for (uint32_t k = 0; k < 8; k++) r += k < w ? infw_popc(n.bm[k]) : 0u;
+    r -= 1;  // bit 0 is always set, so r >= 0
+    if (n.nv <= INFW_NODE_INLINE) {
+        uint32_t v = n.v[0];
+        for (uint32_t k = 1; k < INFW_NODE_INLINE; k++) v = r == k ? n.v[k] : v;
+        return v;
+    }
+    return t.vpool[n.base + r];
+}
+
+template <class T>
+INFW_TD uint32_t infw_dir24_lookup(const T &t, uint32_t slot, uint32_t a32) {
     uint32_t e = t.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
     if (e & INFW_TBL8_FLAG) e = t.tbl8[((uint64_t)(e & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu)];
+    return e;
+}
+
+template <class T>
+INFW_TD uint32_t infw_dir_lookup(const T &t, uint32_t slot, uint32_t a32) {
+    uint32_t e = t.l16[((uint64_t)slot << 16) | (a32 >> 16)];
+    if (e & INFW_NODE_FLAG) {
+        e = infw_node_child(t, t.nodes[e & ~INFW_NODE_FLAG], (a32 >> 8) & 0xFFu);
+        if (e & INFW_NODE_FLAG) e = infw_node_child(t, t.nodes[e & ~INFW_NODE_FLAG], a32 & 0xFFu);
+    }
     return e;
 }
 

@@ -438,41 +438,96 @@ int compile_tables(const PendingMap &m, HostTables &out) {
     }
     out.n_entries = m.nodes.size();
 
-    // --- DIR-24-8 over the unified 32-bit prefix space, per slot
-    if (out.n_slots) {
-        out.tbl24.assign((size_t)out.n_slots << 24, 0u);
-        std::sort(shorts.begin(), shorts.end(),
-                  [](const ShortEnt &a, const ShortEnt &b) { return a.plen < b.plen; });
-        for (const ShortEnt &e : shorts) {
-            uint32_t *t24 = &out.tbl24[(size_t)e.slot << 24];
-            if (e.plen <= 24) {
-                uint32_t start = e.a32 >> 8;
-                uint32_t cnt = 1u << (24 - e.plen);
-                // shorter prefixes were written first; no tbl8 group exists yet
-                std::fill(t24 + start, t24 + start + cnt, e.list1);
-            } else {
-                uint32_t i24 = e.a32 >> 8;
-                uint32_t w = t24[i24];
-                uint32_t g;
-                if (w & INFW_TBL8_FLAG) {
-                    g = w & ~INFW_TBL8_FLAG;
-                } else {
-                    g = (uint32_t)(out.tbl8.size() >> 8);
-                    if (g >= INFW_TBL8_FLAG) {
-                        set_error("compile: tbl8 groups exhausted");
-                        return -ENOSPC;
-                    }
-                    out.tbl8.resize(out.tbl8.size() + 256, w);
-                    t24[i24] = INFW_TBL8_FLAG | g;
+    // --- short table: per slot, a DIR-24-8 build image (shorter prefixes written
+    // first, longer ones overwrite; /25-/32 in 256-entry tbl8 groups) compressed
+    // into l16 words + 64-B run-bitmap nodes (infw_tables.h)
+    std::sort(shorts.begin(), shorts.end(), [](const ShortEnt &a, const ShortEnt &b) {
+        return a.slot != b.slot ? a.slot < b.slot : a.plen < b.plen;
+    });
+    out.l16.assign((size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
+    {
+        std::vector<uint32_t> t24, t8;
+        // node for 256 values; returns the word for the parent (plain value or node ref)
+        auto make_node = [&](const uint32_t *vals) -> uint32_t {
+            bool uniform = true;
+            for (int i = 1; i < 256 && uniform; i++) uniform = vals[i] == vals[0];
+            if (uniform) return vals[0];
+            infw_bnode n;
+            memset(&n, 0, sizeof(n));
+            std::vector<uint32_t> runs;
+            for (int i = 0; i < 256; i++)
+                if (i == 0 || vals[i] != vals[i - 1]) {
+                    n.bm[i >> 5] |= 1u << (i & 31);
+                    runs.push_back(vals[i]);
                 }
-                uint32_t start = e.a32 & 0xFFu, cnt = 1u << (32 - e.plen);
-                std::fill(out.tbl8.begin() + ((size_t)g << 8) + start,
-                          out.tbl8.begin() + ((size_t)g << 8) + start + cnt, e.list1);
+            n.nv = (uint32_t)runs.size();
+            if (n.nv <= INFW_NODE_INLINE) {
+                for (uint32_t k = 0; k < n.nv; k++) n.v[k] = runs[k];
+            } else {
+                n.base = (uint32_t)out.vpool.size();
+                out.vpool.insert(out.vpool.end(), runs.begin(), runs.end());
             }
+            out.nodes.push_back(n);
+            return INFW_NODE_FLAG | (uint32_t)(out.nodes.size() - 1);
+        };
+        size_t si = 0;
+        for (uint32_t slot = 0; slot < out.n_slots; slot++) {
+            size_t sj = si;
+            while (sj < shorts.size() && shorts[sj].slot == slot) sj++;
+            if (sj == si) continue;
+            t24.assign((size_t)1 << 24, 0u);
+            t8.clear();
+            for (size_t x = si; x < sj; x++) {
+                const ShortEnt &e = shorts[x];
+                if (e.plen <= 24) {
+                    uint32_t start = e.a32 >> 8, cnt = 1u << (24 - e.plen);
+                    std::fill(t24.begin() + start, t24.begin() + start + cnt, e.list1);
+                } else {
+                    uint32_t i24 = e.a32 >> 8, w = t24[i24], g;
+                    if (w & INFW_TBL8_FLAG) {
+                        g = w & ~INFW_TBL8_FLAG;
+                    } else {
+                        g = (uint32_t)(t8.size() >> 8);
+                        t8.resize(t8.size() + 256, w);
+                        t24[i24] = INFW_TBL8_FLAG | g;
+                    }
+                    uint32_t start = e.a32 & 0xFFu, cnt = 1u << (32 - e.plen);
+                    std::fill(t8.begin() + ((size_t)g << 8) + start, t8.begin() + ((size_t)g << 8) + start + cnt,
+                              e.list1);
+                }
+            }
+            // keep the DIR-24-8 image (A/B alternative of the compressed form)
+            if (out.tbl24.empty()) out.tbl24.assign((size_t)out.n_slots << 24, 0u);
+            {
+                const uint32_t gbase = (uint32_t)(out.tbl8.size() >> 8);
+                for (size_t k = 0; k < ((size_t)1 << 24); k++) {
+                    uint32_t w = t24[k];
+                    out.tbl24[((size_t)slot << 24) + k] = (w & INFW_TBL8_FLAG) ? (INFW_TBL8_FLAG | (gbase + (w & ~INFW_TBL8_FLAG))) : w;
+                }
+                out.tbl8.insert(out.tbl8.end(), t8.begin(), t8.end());
+            }
+            out.n_tbl8_groups += t8.size() >> 8;
+            uint32_t *l16 = &out.l16[(size_t)slot << 16];
+            uint32_t vals[256];
+            for (uint32_t b = 0; b < 65536; b++) {
+                const uint32_t *blk = &t24[(size_t)b << 8];
+                for (int i = 0; i < 256; i++) {
+                    uint32_t w = blk[i];
+                    vals[i] = (w & INFW_TBL8_FLAG) ? make_node(&t8[(size_t)(w & ~INFW_TBL8_FLAG) << 8]) : w;
+                }
+                l16[b] = make_node(vals);
+                if (out.nodes.size() >= INFW_NODE_FLAG) {
+                    set_error("compile: short-table nodes exhausted");
+                    return -ENOSPC;
+                }
+            }
+            si = sj;
         }
     }
     if (out.tbl24.empty()) out.tbl24.push_back(0);
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
+    if (out.nodes.empty()) out.nodes.push_back(infw_bnode{});
+    if (out.vpool.empty()) out.vpool.push_back(0);
 
     // --- long prefixes: levels, markers, best-matching-prefix
     {
@@ -588,8 +643,11 @@ infw_dev_tables HostTables::view() const {
     t.if_slot = if_slot.data();
     t.if_mask = (uint32_t)if_keys.size() - 1;
     t.n_slots = n_slots;
+    t.l16 = l16.data();
     t.tbl24 = tbl24.data();
     t.tbl8 = tbl8.data();
+    t.nodes = nodes.data();
+    t.vpool = vpool.data();
     t.ltab = ltab.data();
     t.lmask = ltab.size() - 1;
     t.btab = btab.data();

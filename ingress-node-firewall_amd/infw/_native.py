@@ -73,6 +73,25 @@ class BatchSoa(C.Structure):
                 ("meta", C.c_void_p), ("l4word", C.c_void_p)]
 
 
+class EventHdrSt(C.Structure):
+    """struct event_hdr_st (ingress_node_firewall.h:58-64), 8 B packed."""
+    _pack_ = 1
+    _fields_ = [("ifId", C.c_uint16), ("ruleId", C.c_uint16), ("action", C.c_uint8), ("pad", C.c_uint8),
+                ("pktLength", C.c_uint16)]
+
+
+class EventRec(C.Structure):
+    """struct infw_event_rec (include/infw.h), 24 B."""
+    _fields_ = [("hdr", EventHdrSt), ("captured", C.c_uint32), ("reserved", C.c_uint32),
+                ("pkt_index", C.c_uint64)]
+
+
+class ClassifyEx(C.Structure):
+    """struct infw_classify_ex (include/infw.h)."""
+    _fields_ = [("size", C.c_uint32), ("flags", C.c_uint32), ("events", C.c_void_p), ("events_cap", C.c_uint64),
+                ("events_count", C.c_void_p)]
+
+
 class TableInfo(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("n_entries", C.c_uint64), ("n_if_slots", C.c_uint32),
                 ("n_lists", C.c_uint32), ("n_rules", C.c_uint64), ("n_tbl8_groups", C.c_uint64),
@@ -86,7 +105,7 @@ assert C.sizeof(RulesValSt) == 1200 and C.sizeof(RuleStatisticsSt) == 32
 
 # Every symbol include/infw.h declares (checked by tests/test_abi_cpu.py).
 ABI_SYMBOLS = [
-    "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
+    "infw_classify_ex", "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
     "infw_table_delete", "infw_table_get_next_key", "infw_table_lookup", "infw_table_count",
     "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
@@ -126,6 +145,8 @@ _sig = {
     "infw_table_commit": (C.c_int, [C.c_void_p]),
     "infw_classify": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
                                 C.c_void_p]),
+    "infw_classify_ex": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
+                                   P(ClassifyEx), C.c_void_p]),
     "infw_stats_read": (C.c_int, [C.c_void_p, C.c_uint32, P(RuleStatisticsSt), P(C.c_int)]),
     "infw_stats_read_all": (C.c_int, [C.c_void_p, P(RuleStatisticsSt)]),
     "infw_stats_reset": (C.c_int, [C.c_void_p]),
@@ -200,3 +221,5 @@ for _name, (_res, _args) in _wsig.items():
     _f = getattr(wl, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+assert C.sizeof(EventHdrSt) == 8 and C.sizeof(EventRec) == 24

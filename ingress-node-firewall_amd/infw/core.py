@@ -155,6 +155,23 @@ class Classifier:
                            results.data_ptr() if results is not None else 0,
                            verdicts.data_ptr() if verdicts is not None else 0, sp)
 
+    def classify_events(self, batch, events, events_count, results=None, verdicts=None, dev: int = 0,
+                        stream=None) -> None:
+        """classify + the deny-event stream (kernel.c:392-399) into `events` (uint8 tensor of cap*24 B)
+        and `events_count` (int64 tensor [1], incremented by the kernel)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(batch.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        b = N.BatchSoa(batch.saddr.data_ptr(), batch.ifindex.data_ptr(), batch.pkt_len.data_ptr(),
+                       batch.meta.data_ptr(), batch.l4word.data_ptr())
+        ex = N.ClassifyEx(C.sizeof(N.ClassifyEx), 0, events.data_ptr(), events.numel() // C.sizeof(N.EventRec),
+                          events_count.data_ptr())
+        check(N.lib.infw_classify_ex(self._ctx, dev, C.byref(b), batch.n,
+                                     results.data_ptr() if results is not None else None,
+                                     verdicts.data_ptr() if verdicts is not None else None, C.byref(ex), sp),
+              "classify_ex")
+
     def set_launch(self, block: int = 512, scan_group: int = 0, blocks_per_cu: int = 4) -> None:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
         check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")

@@ -38,6 +38,11 @@ for _n, (_r, _a) in _sig.items():
     getattr(_lib, _n).restype = _r
     getattr(_lib, _n).argtypes = _a
 
+class OrcEvent(C.Structure):
+    _fields_ = [("pkt_index", C.c_uint64), ("ifId", C.c_uint16), ("ruleId", C.c_uint16), ("action", C.c_uint8),
+                ("pad", C.c_uint8), ("pktLength", C.c_uint16), ("captured", C.c_uint16)]
+
+
 STATS_DTYPE = np.uint64  # [1024, 4]: allow.packets, allow.bytes, deny.packets, deny.bytes
 
 
@@ -113,3 +118,21 @@ class OracleMap:
                                         None if res is None else res.ctypes.data,
                                         None if ver is None else ver.ctypes.data, stats.ctypes.data, nthreads)
         return res, ver, stats, secs
+
+    def collect_events(self, hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifindex: np.ndarray,
+                       max_events: int | None = None):
+        """DENY events (kernel.c:392-399) in packet order: array of (pkt_index, ifId, ruleId, action, pktLength,
+        captured)."""
+        n = hdr.shape[0]
+        h = np.ascontiguousarray(hdr, dtype=np.uint8)
+        w = h.shape[1] if n else 0
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(w)
+        cap = np.ascontiguousarray(caplen, np.uint32)
+        pl = np.ascontiguousarray(pkt_len, np.uint32)
+        ifx = np.ascontiguousarray(ifindex, np.uint32)
+        m = n if max_events is None else max_events
+        ev = (OrcEvent * max(m, 1))()
+        k = _lib.orc_collect_events(self._m, h.ctypes.data, offs.ctypes.data, cap.ctypes.data, pl.ctypes.data,
+                                    ifx.ctypes.data, n, ev, m)
+        return np.array([(e.pkt_index, e.ifId, e.ruleId, e.action, e.pktLength, e.captured) for e in ev[:k]],
+                        dtype=np.uint64).reshape(-1, 6)

@@ -157,3 +157,47 @@ def test_full_size_properties():
         ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
         got = res1[start:start + (1 << 16)].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, ores), start
+
+
+def _gpu_events(clf, batch, cap):
+    import ctypes as C
+    from infw import _native as N
+    ev = torch.zeros(cap * C.sizeof(N.EventRec), dtype=torch.uint8, device=batch.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=batch.device)
+    res = torch.empty(batch.n, dtype=torch.int32, device=batch.device)
+    clf.classify_events(batch, ev, cnt, results=res)
+    torch.cuda.synchronize()
+    raw = ev.cpu().numpy().view(np.uint64).reshape(-1, 3)
+    k = min(int(cnt.item()), cap)
+    h = raw[:k, 0]
+    rec = np.stack([raw[:k, 2], h & 0xFFFF, (h >> 16) & 0xFFFF, (h >> 32) & 0xFF, h >> 48, raw[:k, 1]], axis=1)
+    return rec, int(cnt.item()), res.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG2_MIXED_1M, 50000, 256), (W.CFG4_ADVERSARIAL, 20000, 64)])
+def test_deny_events_match_oracle(cfg, npfx, ntmpl):
+    """Deny-event stream (kernel.c:392-399): one record per rule DROP, identical to the oracle's perf records
+    (event_hdr_st fields, captured length, packet index); overflow counts lost records like perf."""
+    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    n = 1 << 18
+    dev = torch.device("cuda", 0)
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 4242, 0)
+    hdr, cap, pl, ifx = wl.frames(4242, n)
+    want = m.collect_events(hdr, cap, pl, ifx)
+    assert want.shape[0] > 1000
+    got, count, res = _gpu_events(clf, batch, n)
+    assert count == want.shape[0]
+    got = got[np.argsort(got[:, 0], kind="stable")]
+    assert np.array_equal(got, want)
+    ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(res, ores)
+    # a ring smaller than the event count: every record written is a real event, the count is exact
+    small, count2, _ = _gpu_events(clf, batch, 1000)
+    assert count2 == want.shape[0] and small.shape[0] == 1000
+    wset = {tuple(r) for r in want.tolist()}
+    assert all(tuple(r) in wset for r in small.tolist())
