@@ -133,3 +133,55 @@ def test_update_delete_churn_matches_oracle():
         c.commit()
         res, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
         assert np.array_equal(c.debug_walk(tup), res), step
+
+
+def test_decision_tables_exhaustive_values():
+    """Every 16-bit packet value for every packet class of random 100-slot rule lists: the compiled
+    first-match decision tables (and, inside infw_debug_walk, the serial class-list scan) equal the
+    oracle's scan of the raw rulesVal_st."""
+    rng = random.Random(3)
+    import goenc
+    from frames import frame, snapshots
+    ents = []
+    for t in range(6):
+        rules = []
+        for slot in range(1, 100):
+            if rng.random() < 0.35:
+                continue
+            proto = rng.choice([6, 6, 17, 17, 132, 1, 58, 0, 47]) if slot > 60 or rng.random() < 0.97 else 0
+            ps = rng.randrange(0, 65536)
+            kind = rng.random()
+            pe = 0 if kind < 0.4 else min(65535, ps + rng.randrange(1, 4000)) if kind < 0.9 else rng.randrange(0, 65536)
+            rules.append({"slot": slot, "ruleId": slot, "protocol": proto, "dstPortStart": ps, "dstPortEnd": pe,
+                          "icmpType": rng.randrange(256), "icmpCode": rng.randrange(256),
+                          "action": rng.choice([1, 2])})
+        ents.append((goenc.build_key(9, f"10.{t}.0.0/16"), goenc.raw_value(rules)))
+        ents.append((goenc.build_key(9, f"2001:db8:{t}::/48"), goenc.raw_value(rules)))
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    m = orc.OracleMap()
+    for k, v in ents:
+        c.update(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v))
+        assert m.update(k, v) == 0
+    c.commit()
+    vals = np.arange(65536, dtype=np.uint32)
+    for t in range(6):
+        for src, proto in ((f"10.{t}.1.1", 6), (f"10.{t}.1.1", 17), (f"10.{t}.1.1", 132), (f"10.{t}.1.1", 1),
+                           (f"10.{t}.1.1", 58), (f"2001:db8:{t}::9", 6), (f"2001:db8:{t}::9", 58),
+                           (f"2001:db8:{t}::9", 1), (f"2001:db8:{t}::9", 132)):
+            base = frame(src, proto=proto, dport=0, length=100)
+            tup = np.repeat(W.pack_frames(*snapshots([base]), np.array([9], np.uint32)), 65536, axis=0)
+            if proto in (1, 58):
+                tup[:, 7] = (vals >> 8) | ((vals & 0xFF) << 8)          # l4word bytes 0,1 = type, code
+            else:
+                tup[:, 7] = ((vals >> 8) << 16) | ((vals & 0xFF) << 24)  # bytes 2,3 = dport (network order)
+            got = c.debug_walk(tup)
+            # oracle on the same 65536 frames
+            hdr = np.repeat(snapshots([base])[0], 65536, axis=0)
+            off = 34 if "." in src else 54
+            if proto in (1, 58):
+                hdr[:, off], hdr[:, off + 1] = vals >> 8, vals & 0xFF
+            else:
+                hdr[:, off + 2], hdr[:, off + 3] = vals >> 8, vals & 0xFF
+            n = np.full(65536, 100, np.uint32)
+            want, _, _, _ = m.classify_frames(hdr, n, n, np.full(65536, 9, np.uint32), nthreads=4)
+            assert np.array_equal(got, want), (t, src, proto, np.nonzero(got != want)[0][:5])
