@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <chrono>
 #include <memory>
@@ -118,6 +119,7 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;
     t.bmask = h.btab.size() - 1;
+    t.short_mode = h.short_mode;
     t.n_levels = (uint32_t)h.levels.size();
     out = ep;
     return 0;
@@ -251,7 +253,9 @@ int infw_table_commit(infw_ctx *ctx) {
     if (!ctx) return -EINVAL;
     auto t0 = std::chrono::steady_clock::now();
     HostTables h;
-    int rc = compile_tables(ctx->map, h);
+    int mode = -1;
+    if (const char *e = getenv("INFW_SHORT_TABLE")) mode = strcmp(e, "compressed") == 0 ? 1 : strcmp(e, "dir24") == 0 ? 0 : -1;
+    int rc = compile_tables(ctx->map, h, mode);
     if (rc) return rc;
     auto t1 = std::chrono::steady_clock::now();
     std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size());

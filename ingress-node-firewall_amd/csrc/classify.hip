@@ -160,13 +160,10 @@ __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel
                     // long prefix covers the address (the kernel is bound by random
                     // memory traffic, not latency: no speculative short-table fetch)
                     uint32_t lng = 0, sh = 0;
-                    // A/B flags: 32 = DIR-24-8 image instead of the compressed table,
-                    // 64 = fetch the short table before (beside) the IPv6 bucket
-                    if (kAblate & 64) sh = (kAblate & 32) ? infw_dir24_lookup(T, (uint32_t)slot, a32)
-                                                          : infw_dir_lookup(T, (uint32_t)slot, a32);
+                    // diagnostic 64: fetch the short table beside the IPv6 bucket (speculative)
+                    if (kAblate & 64) sh = infw_short_lookup(T, (uint32_t)slot, a32);
                     if (pk == INFW_PK_V6 && T.n_levels) lng = infw_v6_long(T, (uint32_t)slot, a32, sw);
-                    if (!(kAblate & 64) && !lng)
-                        sh = (kAblate & 32) ? infw_dir24_lookup(T, (uint32_t)slot, a32) : infw_dir_lookup(T, (uint32_t)slot, a32);
+                    if (!(kAblate & 64) && !lng) sh = infw_short_lookup(T, (uint32_t)slot, a32);
                     l1 = lng ? lng : sh;
                 }
             }
@@ -296,11 +293,7 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         case 4: launch<512, 0, 4>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 8: launch<512, 0, 8>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 3: launch<512, 0, 3>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 32: launch<512, 0, 32>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 96: launch<512, 0, 96>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 34: launch<512, 0, 34>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 98: launch<512, 0, 98>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;

@@ -71,7 +71,8 @@ struct HostTables {
     std::vector<infw_bnode> nodes;
     std::vector<uint32_t> vpool;
     uint64_t n_tbl8_groups = 0;   // DIR-24-8 second-level groups of the build image
-    std::vector<uint32_t> tbl24, tbl8;  // the DIR-24-8 image itself (kept for A/B)
+    std::vector<uint32_t> tbl24, tbl8;  // DIR-24-8 form (short_mode == INFW_SHORT_DIR24)
+    uint32_t short_mode = INFW_SHORT_DIR24;
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;
     uint64_t n_buckets = 0, n_overflow_groups = 0;
@@ -87,7 +88,9 @@ struct HostTables {
     infw_dev_tables view() const;
 };
 
-int compile_tables(const PendingMap &m, HostTables &out);
+// short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
+int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,
+                   uint64_t dir24_budget = 4ull << 30);
 
 // Class-filtered GPU rule records of one 1200-B value (appended to rules) and
 // the per-class first-match decision tables (appended to dt).

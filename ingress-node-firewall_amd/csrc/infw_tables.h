@@ -110,8 +110,9 @@ struct infw_dev_tables {
     const uint32_t *l16;       // n_slots << 16
     const struct infw_bnode *nodes;
     const uint32_t *vpool;
-    const uint32_t *tbl24;     // DIR-24-8 image of the same short table (A/B), n_slots << 24
+    const uint32_t *tbl24;     // DIR-24-8 form: n_slots << 24 words + tbl8 groups
     const uint32_t *tbl8;
+    uint32_t short_mode;       // INFW_SHORT_DIR24 or INFW_SHORT_COMPRESSED
     const struct infw_long_entry *ltab;
     uint64_t lmask;
     const struct infw_v6_bucket *btab;
@@ -257,6 +258,11 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
     return t.vpool[n.base + r];
 }
 
+// Short-table form: DIR-24-8 (one 4-B gather, 64 MiB per ifindex) unless that
+// exceeds the memory budget, then the compressed 16-8-8 form (~16 B per prefix).
+#define INFW_SHORT_DIR24 0u
+#define INFW_SHORT_COMPRESSED 1u
+
 template <class T>
 INFW_TD uint32_t infw_dir24_lookup(const T &t, uint32_t slot, uint32_t a32) {
     uint32_t e = t.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
@@ -327,6 +333,11 @@ INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uin
     }
 }
 
+template <class T>
+INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
+    return t.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(t, slot, a32) : infw_dir_lookup(t, slot, a32);
+}
+
 // list+1 of the longest matching entry, 0 if none.
 template <class T>
 INFW_TD uint32_t infw_lpm(const T &t, int pk, uint32_t ifindex, const uint32_t sa[4]) {
@@ -337,7 +348,7 @@ INFW_TD uint32_t infw_lpm(const T &t, int pk, uint32_t ifindex, const uint32_t s
         uint32_t r = infw_v6_long(t, (uint32_t)slot, a32, sa);
         if (r) return r;
     }
-    return infw_dir_lookup(t, (uint32_t)slot, a32);
+    return infw_short_lookup(t, (uint32_t)slot, a32);
 }
 
 // First match of class list (off, cnt) against value v (serial form).

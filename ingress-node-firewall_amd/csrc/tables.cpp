@@ -350,7 +350,7 @@ struct ShortEnt {
 };
 }  // namespace
 
-int compile_tables(const PendingMap &m, HostTables &out) {
+int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uint64_t dir24_budget) {
     out = HostTables();
     // --- slots: distinct ifindexes, ascending
     std::vector<uint32_t> ifs;
@@ -444,7 +444,10 @@ int compile_tables(const PendingMap &m, HostTables &out) {
     std::sort(shorts.begin(), shorts.end(), [](const ShortEnt &a, const ShortEnt &b) {
         return a.slot != b.slot ? a.slot < b.slot : a.plen < b.plen;
     });
-    out.l16.assign((size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
+    out.short_mode = short_mode_req >= 0 ? (uint32_t)short_mode_req
+                     : ((uint64_t)out.n_slots << 26) <= dir24_budget ? INFW_SHORT_DIR24 : INFW_SHORT_COMPRESSED;
+    const bool dir24 = out.short_mode == INFW_SHORT_DIR24;
+    out.l16.assign(dir24 ? 1 : (size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
     {
         std::vector<uint32_t> t24, t8;
         // node for 256 values; returns the word for the parent (plain value or node ref)
@@ -496,17 +499,18 @@ int compile_tables(const PendingMap &m, HostTables &out) {
                               e.list1);
                 }
             }
-            // keep the DIR-24-8 image (A/B alternative of the compressed form)
-            if (out.tbl24.empty()) out.tbl24.assign((size_t)out.n_slots << 24, 0u);
-            {
+            out.n_tbl8_groups += t8.size() >> 8;
+            if (dir24) {  // keep the DIR-24-8 image as the device form
+                if (out.tbl24.empty()) out.tbl24.assign((size_t)out.n_slots << 24, 0u);
                 const uint32_t gbase = (uint32_t)(out.tbl8.size() >> 8);
                 for (size_t k = 0; k < ((size_t)1 << 24); k++) {
                     uint32_t w = t24[k];
                     out.tbl24[((size_t)slot << 24) + k] = (w & INFW_TBL8_FLAG) ? (INFW_TBL8_FLAG | (gbase + (w & ~INFW_TBL8_FLAG))) : w;
                 }
                 out.tbl8.insert(out.tbl8.end(), t8.begin(), t8.end());
+                si = sj;
+                continue;
             }
-            out.n_tbl8_groups += t8.size() >> 8;
             uint32_t *l16 = &out.l16[(size_t)slot << 16];
             uint32_t vals[256];
             for (uint32_t b = 0; b < 65536; b++) {
@@ -646,6 +650,7 @@ infw_dev_tables HostTables::view() const {
     t.l16 = l16.data();
     t.tbl24 = tbl24.data();
     t.tbl8 = tbl8.data();
+    t.short_mode = short_mode;
     t.nodes = nodes.data();
     t.vpool = vpool.data();
     t.ltab = ltab.data();

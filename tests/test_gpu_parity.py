@@ -201,3 +201,13 @@ def test_deny_events_match_oracle(cfg, npfx, ntmpl):
     assert count2 == want.shape[0] and small.shape[0] == 1000
     wset = {tuple(r) for r in want.tolist()}
     assert all(tuple(r) in wset for r in small.tolist())
+
+
+def test_parity_compressed_short_table(monkeypatch):
+    """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
+    budget, e.g. many ifindexes) classifies bit-identically."""
+    monkeypatch.setenv("INFW_SHORT_TABLE", "compressed")
+    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
+    assert_parity(r, "cfg2-compressed")
+    r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64)
+    assert_parity(r, "cfg4-compressed")
