@@ -81,8 +81,10 @@ struct EventSink {
     unsigned long long *count;
 };
 
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false>
-__global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
+// kWaves: minimum waves per SIMD the register allocation must allow (8 = four
+// 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6)>
+__global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
@@ -255,14 +257,14 @@ __global__ __launch_bounds__(kBlock, kBlock == 512 ? 8 : 6) void classify_kernel
     }
 }
 
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false>
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6)>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             EventSink ev = EventSink{nullptr, 0, nullptr}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n,
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n,
                        results, verdicts, st, ev);
 }
 
@@ -302,6 +304,7 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
     }
     if (group == 0) {
         if (block == 256) launch<256, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else if (bpc <= 3) launch<512, 0, 0, false, 6>(bpc, cus, T, in, n, results, verdicts, st, stream);
         else launch<512, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
     } else if (block == 256) {
         if (group == 1) launch<256, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
