@@ -12,7 +12,7 @@ OBJ      := $(PKG)/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
 EXTRA    ?=
 
-LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip
+LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip $(SRC)/pack.hip
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 

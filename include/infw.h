@@ -126,6 +126,26 @@ struct infw_batch_soa {
     ((uint32_t)((ethertype) & 0xFFFFu) | ((uint32_t)((proto) & 0xFFu) << 16) | \
      ((uint32_t)((caplen) > 255u ? 255u : (caplen)) << 24))
 
+/* Raw frames in device memory (NIC -> HBM ingestion): frame i */
+/* starts at frames + (offsets ? offsets[i] : i * stride); only its first     */
+/* linear_len[i] bytes are read (xdp data .. data_end).                       */
+struct infw_frame_batch {
+    const uint8_t *frames;
+    const uint64_t *offsets;      /* NULL: fixed-stride chunks (AF_XDP umem style)   */
+    uint64_t stride;
+    const uint32_t *linear_len;   /* data_end - data                                  */
+    const uint32_t *pkt_len;      /* bpf_xdp_get_buff_len(); NULL: = linear_len       */
+    const uint32_t *ifindex;
+};
+/* Writable SoA destination of infw_pack_frames (same layout as infw_batch_soa). */
+struct infw_batch_soa_out {
+    uint8_t *saddr;
+    uint32_t *ifindex;
+    uint32_t *pkt_len;
+    uint32_t *meta;
+    uint32_t *l4word;
+};
+
 typedef struct infw_ctx infw_ctx;
 
 /* ------------------------------------------------------------------------ */
@@ -200,6 +220,11 @@ int infw_classify(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint6
 /* 1|4|8 = one-lane-per-rule ballot scan with that many packets in flight; */
 /* blocks_per_cu resident workgroups per CU.                                  */
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
+
+/* Frame headers -> SoA tuples on the device (the packer of the batch format  */
+/* above, run as a kernel over frames already in HBM).  Asynchronous.          */
+int infw_pack_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
+                     const struct infw_batch_soa_out *out, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */

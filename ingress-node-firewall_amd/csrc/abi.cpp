@@ -17,6 +17,9 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
                                     infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count);
 
+extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
+                                       uint32_t cus, hipStream_t stream);
+
 namespace infw {
 
 static thread_local std::string g_err;
@@ -372,6 +375,28 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
                                   evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr);
     if (rc) {
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    return 0;
+}
+
+int infw_pack_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
+                     void *stream) {
+    if (!ctx || !fb || !out) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("pack_frames: host-only context");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (n && (!fb->frames || !fb->linear_len || !fb->ifindex || (!fb->offsets && !fb->stride) || !out->saddr ||
+              !out->ifindex || !out->pkt_len || !out->meta || !out->l4word || ((uintptr_t)out->saddr & 15))) {
+        set_error("pack_frames: bad arguments");
+        return -EINVAL;
+    }
+    DeviceGuard g(ctx->devs[dev].ordinal);
+    if (!g.ok) return -ENODEV;
+    if (infw_launch_pack_frames(fb, n, out, ctx->devs[dev].cus, static_cast<hipStream_t>(stream))) {
+        set_error(std::string("pack launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
     return 0;

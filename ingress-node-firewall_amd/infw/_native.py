@@ -73,6 +73,12 @@ class BatchSoa(C.Structure):
                 ("meta", C.c_void_p), ("l4word", C.c_void_p)]
 
 
+class FrameBatch(C.Structure):
+    """struct infw_frame_batch (include/infw.h)."""
+    _fields_ = [("frames", C.c_void_p), ("offsets", C.c_void_p), ("stride", C.c_uint64), ("linear_len", C.c_void_p),
+                ("pkt_len", C.c_void_p), ("ifindex", C.c_void_p)]
+
+
 class EventHdrSt(C.Structure):
     """struct event_hdr_st (ingress_node_firewall.h:58-64), 8 B packed."""
     _pack_ = 1
@@ -105,7 +111,7 @@ assert C.sizeof(RulesValSt) == 1200 and C.sizeof(RuleStatisticsSt) == 32
 
 # Every symbol include/infw.h declares (checked by tests/test_abi_cpu.py).
 ABI_SYMBOLS = [
-    "infw_classify_ex", "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
+    "infw_classify_ex", "infw_pack_frames", "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
     "infw_table_delete", "infw_table_get_next_key", "infw_table_lookup", "infw_table_count",
     "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
@@ -147,6 +153,7 @@ _sig = {
                                 C.c_void_p]),
     "infw_classify_ex": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
                                    P(ClassifyEx), C.c_void_p]),
+    "infw_pack_frames": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoa), C.c_void_p]),
     "infw_stats_read": (C.c_int, [C.c_void_p, C.c_uint32, P(RuleStatisticsSt), P(C.c_int)]),
     "infw_stats_read_all": (C.c_int, [C.c_void_p, P(RuleStatisticsSt)]),
     "infw_stats_reset": (C.c_int, [C.c_void_p]),

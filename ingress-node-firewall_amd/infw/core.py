@@ -172,6 +172,20 @@ class Classifier:
                                      verdicts.data_ptr() if verdicts is not None else None, C.byref(ex), sp),
               "classify_ex")
 
+    def pack_frames(self, frames, linear_len, ifindex, out, pkt_len=None, offsets=None, stride: int = 0,
+                    dev: int = 0, stream=None) -> None:
+        """Frames in device memory (uint8 tensor) -> the SoA batch `out` on the device (§8f-3)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        fb = N.FrameBatch(frames.data_ptr(), offsets.data_ptr() if offsets is not None else None, stride,
+                          linear_len.data_ptr(), pkt_len.data_ptr() if pkt_len is not None else None,
+                          ifindex.data_ptr())
+        o = N.BatchSoa(out.saddr.data_ptr(), out.ifindex.data_ptr(), out.pkt_len.data_ptr(), out.meta.data_ptr(),
+                       out.l4word.data_ptr())
+        check(N.lib.infw_pack_frames(self._ctx, dev, C.byref(fb), out.n, C.byref(o), sp), "pack_frames")
+
     def set_launch(self, block: int = 512, scan_group: int = 0, blocks_per_cu: int = 4) -> None:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
         check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")

@@ -211,3 +211,44 @@ def test_parity_compressed_short_table(monkeypatch):
     assert_parity(r, "cfg2-compressed")
     r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64)
     assert_parity(r, "cfg4-compressed")
+
+
+def test_pack_frames_on_device():
+    """§8f-3 raw-frame ingestion: frames in HBM (fixed-stride chunks, and back-to-back variable-length frames
+    with an offset array) packed on the GPU equal the host packer's tuples; classifying them matches the oracle."""
+    from frames import frame, snapshots
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 1 << 18
+    hdr, cap, pl, ifx = wl.frames(99, n)
+    t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    out = SoaBatch.empty(n, dev)
+    clf.pack_frames(torch.from_numpy(hdr).to(dev), t(np.minimum(cap, 80)), t(ifx), out, pkt_len=t(pl), stride=80)
+    torch.cuda.synchronize()
+    want = W.pack_frames(hdr, np.minimum(cap, 80), pl, ifx)
+    assert np.array_equal(out.to_tuples(), want)
+    gres, gver = gpu_run(clf, out, n)
+    ores, over, _, _ = m.classify_frames(hdr, np.minimum(cap, 80), pl, ifx, nthreads=8)
+    assert np.array_equal(gres, ores) and np.array_equal(gver, over)
+    # variable-length real frames, back to back, the shortest at the very end of the buffer
+    rng = np.random.default_rng(5)
+    fr = []
+    for k in range(3000):
+        src = "1.1.%d.%d" % (k & 255, (k >> 8) & 255) if k % 2 else "100:1::%x" % k
+        f = frame(src, proto=["tcp", "udp", "icmp", "icmpv6", "sctp", "gre"][k % 6], dport=int(rng.integers(0, 65536)),
+                  icmp_type=8, length=int(rng.integers(40, 300)))
+        fr.append(f[: int(rng.integers(0, len(f) + 1))] if k % 7 == 0 else f)
+    fr.append(frame("1.1.1.1", proto="tcp", dport=150)[:15])
+    offs = np.cumsum([0] + [len(f) for f in fr[:-1]]).astype(np.uint64)
+    buf = torch.from_numpy(np.frombuffer(b"".join(fr), np.uint8).copy()).to(dev)
+    lens = np.array([len(f) for f in fr], np.uint32)
+    ifs = np.ones(len(fr), np.uint32)
+    out2 = SoaBatch.empty(len(fr), dev)
+    clf.pack_frames(buf, t(lens), t(ifs), out2, offsets=torch.from_numpy(offs.view(np.int64)).to(dev))
+    torch.cuda.synchronize()
+    h2, c2, p2 = snapshots(fr)
+    assert np.array_equal(out2.to_tuples(), W.pack_frames(h2, c2, p2, ifs))
