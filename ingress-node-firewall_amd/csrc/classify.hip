@@ -83,7 +83,8 @@ struct EventSink {
 
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6)>
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
+          bool kPrefetch = !(kAblate & 128)>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -109,12 +110,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t *__restrict__ rules = T.rules;
 
-    for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        const bool valid = i < n;
-        uint32_t meta = 0, l4w = 0, ifx = 0, plen = 0;
-        uint4 sa = make_uint4(0, 0, 0, 0);
-        if (valid) {
+    // the next tile's tuple is loaded while the current tile walks the tables:
+    // the stream's latency overlaps the first table lookups instead of adding to them
+    auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa) {
+        if (i < n) {
             if (!(kAblate & 16)) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL (16: plain, diagnostic)
                 meta = __builtin_nontemporal_load(&in.meta[i]);
                 l4w = __builtin_nontemporal_load(&in.l4word[i]);
@@ -130,6 +129,18 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 sa = sa4[i];
             }
         }
+    };
+    uint32_t n_meta = 0, n_l4w = 0, n_ifx = 0, n_plen = 0;
+    uint4 n_sa = make_uint4(0, 0, 0, 0);
+    load_tuple((uint64_t)blockIdx.x * kBlock + threadIdx.x, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        if (!kPrefetch && base != (uint64_t)blockIdx.x * kBlock) load_tuple(i, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+        const uint32_t meta = valid ? n_meta : 0, l4w = n_l4w, ifx = n_ifx, plen = n_plen;
+        const uint4 sa = n_sa;
+        if (kPrefetch) load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         int cls = 0;
         uint32_t val = 0;
         const int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
@@ -212,6 +223,30 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         // ---- verdict (kernel.c:444-456) and statistics (kernel.c:376-387)
         const uint32_t action = result & 0xFFu;
         const uint32_t key = (result >> 8) & 0xFFFFu;
+        if (!(kAblate & 4)) {
+            // counter slot of this packet, or -1 (no stats: UNDEF, action outside {1,2}, key >= 1024)
+            const int s = (valid && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
+                              ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
+            // per-wavefront aggregation of the most common slot (Zipf traffic: the first eligible
+            // lane's slot): its lanes are summed in registers and added once; the rest go to LDS
+            const uint64_t elig = __ballot(s >= 0);
+            if (elig) {
+                const int lead = __builtin_ctzll(elig);
+                const int s0 = __builtin_amdgcn_readlane(s, lead);
+                const bool mine = s == s0;
+                const uint64_t grp = __ballot(mine);
+                unsigned long long by = mine ? (unsigned long long)plen : 0ull;
+                for (int off = 32; off > 0; off >>= 1) by += __shfl_xor(by, off);
+                if (lane == lead) {
+                    atomicAdd(&s_pk[s0], (uint32_t)__popcll(grp));
+                    atomicAdd(&s_by[s0], by);
+                }
+                if (s >= 0 && !mine) {
+                    atomicAdd(&s_pk[s], 1u);
+                    atomicAdd(&s_by[s], (unsigned long long)plen);
+                }
+            }
+        }
         if (kEvents) {  // deny events (kernel.c:392-399): one atomic per wave, lanes keep their order
             const bool deny = valid && action == INFW_XDP_DROP;
             const uint64_t m = __ballot(deny);
@@ -238,11 +273,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             }
             if (verdicts)
                 verdicts[i] = (pk == INFW_PK_DROP_SHORT || action == INFW_XDP_DROP) ? INFW_XDP_DROP : INFW_XDP_PASS;
-            if (!(kAblate & 4) && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys) {
-                const int s = (int)key * 2 + (action == INFW_XDP_DROP);
-                atomicAdd(&s_pk[s], 1u);
-                atomicAdd(&s_by[s], (unsigned long long)plen);
-            }
+
         }
     }
 
@@ -295,6 +326,7 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         case 4: launch<512, 0, 4>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 8: launch<512, 0, 8>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 3: launch<512, 0, 3>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 128: launch<512, 0, 128>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
