@@ -42,7 +42,14 @@ asm:
 	@mkdir -p $(OBJ)/asm
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S -o $(OBJ)/asm/classify.s $(SRC)/classify.hip
 
+# host-only sanitizer run of the table compiler + shared walk (no GPU code involved)
+asan:
+	@mkdir -p $(OBJ)
+	g++ -std=c++17 -g -O1 -fsanitize=address,undefined -fno-sanitize-recover=undefined -Iinclude \
+	    tools/asan_walk.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp -o $(OBJ)/asan_walk
+	$(OBJ)/asan_walk
+
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build
 
-.PHONY: all clean resource-usage asm
+.PHONY: all clean resource-usage asm asan

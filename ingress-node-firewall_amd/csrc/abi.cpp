@@ -116,7 +116,7 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
         (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
         (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.btab, &t.btab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
         (rc = upload(*ep, h.rules, &t.rules)) ||
-        (rc = upload(*ep, h.ddesc, &t.ddesc)) || (rc = upload(*ep, h.dt, &t.dt)) || (rc = upload(*ep, h.levels, &t.levels)))
+        (rc = upload(*ep, h.dte, &t.dte)) || (rc = upload(*ep, h.dtl, &t.dtl)) || (rc = upload(*ep, h.levels, &t.levels)))
         return rc;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.n_slots = h.n_slots;
@@ -313,7 +313,7 @@ int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t 
             uint32_t l1 = infw_lpm(t, pk, q[4], q);
             if (l1) {
                 const uint64_t row = (uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls;
-                result = infw_dt_eval(t, t.ddesc[row], val);
+                result = infw_dt_eval(t, l1 - 1, cls, val);
                 const uint32_t scan = infw_scan_serial(t, t.desc[row], val);
                 if (scan != result) {
                     set_error("debug_walk: decision table disagrees with the rule scan");

@@ -55,23 +55,36 @@ __device__ __forceinline__ uint32_t scan_tail(const uint64_t *__restrict__ rules
     return 0;
 }
 
-// First-match result from a decision table (infw_tables.h), one lane per packet:
-// <= 3 dependent 16-B node loads (8 u16 keys each) and one result load.
-__device__ __forceinline__ uint32_t dt_eval(const uint32_t *__restrict__ dt, uint64_t dd, uint32_t v) {
-    const uint32_t S = (uint32_t)(dd >> 32) & 0xFFFFu;
-    if (S <= 1) return S ? (uint32_t)dd : 0u;
-    const uint32_t d = (uint32_t)(dd >> 48) & 0xFFu;
-    const uint4 *base = reinterpret_cast<const uint4 *>(dt) + (uint32_t)dd;
-    uint32_t node = 0, lvl = 0, span = d == 1 ? 9u : d == 2 ? 81u : 729u;
-    for (uint32_t l = 0; l < d; l++) {
-        const uint4 k = base[lvl + node];
-        const uint32_t c = infw_count_lt(k.x, v) + infw_count_lt(k.y, v) + infw_count_lt(k.z, v) +
-                           infw_count_lt(k.w, v);
-        lvl += (S + span - 1) / span;
-        span /= 9u;
-        node = node * 9u + c;
+// First-match result from the decision-table lines of (list, cls) (infw_tables.h),
+// one lane per packet: the entry line, and for S > 10 one leaf line, each read
+// whole (four 16-B loads of one 64-B line, issued back to back).
+__device__ __forceinline__ uint32_t lt2(uint32_t w, uint32_t v) { return infw_count_lt(w, v); }
+__device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
+                                              uint32_t list, int cls, uint32_t v) {
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + ((uint64_t)list * INFW_NCLS + (uint32_t)cls));
+    u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
+    if (a[0] & INFW_DT_ROOT) {
+        const uint32_t g = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
+                           lt2(b[3], v) + lt2(c[0], v) + lt2(c[1], v) + lt2(c[2], v) + lt2(c[3], v) + lt2(d[0], v) +
+                           lt2(d[1], v) + lt2(d[2], v) + lt2(d[3], v);
+        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & ~INFW_DT_ROOT) + g));
+        a = l[0];
+        b = l[1];
+        c = l[2];
+        d = l[3];
     }
-    return reinterpret_cast<const uint32_t *>(base + lvl)[node];
+    const uint32_t k = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v);
+    uint32_t r = b[2];
+    r = k >= 1 ? b[3] : r;
+    r = k >= 2 ? c[0] : r;
+    r = k >= 3 ? c[1] : r;
+    r = k >= 4 ? c[2] : r;
+    r = k >= 5 ? c[3] : r;
+    r = k >= 6 ? d[0] : r;
+    r = k >= 7 ? d[1] : r;
+    r = k >= 8 ? d[2] : r;
+    r = k >= 9 ? d[3] : r;
+    return r;
 }
 
 // G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
@@ -144,7 +157,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         int cls = 0;
         uint32_t val = 0;
         const int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
-        uint64_t d = 0;
+        uint64_t d = 0;    // ballot mode: class-list descriptor
+        uint32_t lst = 0;  // decision mode: list + 1 (0: no LPM entry)
         if (kAblate & 8) {  // diagnostic: input stream + output only
             if (valid && results) results[i] = meta ^ l4w ^ sa.x ^ sa.y ^ sa.z ^ sa.w ^ ifx ^ plen;
             continue;
@@ -180,13 +194,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     l1 = lng ? lng : sh;
                 }
             }
-            if (l1) d = (G == 0 ? T.ddesc : T.desc)[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
+            if (G == 0) lst = l1;
+            else if (l1) d = T.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
         }
         const uint32_t off = (uint32_t)d, cnt = (uint32_t)(d >> 32);
 
         uint32_t result = 0;
-        if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32);  // diagnostic 2: no first-match stage
-        else if (G == 0 && d) result = dt_eval(T.dt, d, val);
+        if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32) ^ lst;  // diagnostic 2: no first-match stage
+        else if (G == 0 && lst) result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val);
         // ---- first match, one lane per rule, G packets in flight
         uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
         while (G > 0 && pending) {

@@ -79,8 +79,7 @@ struct HostTables {
     std::vector<uint8_t> levels;
     std::vector<uint64_t> desc;
     std::vector<uint64_t> rules;
-    std::vector<uint64_t> ddesc;
-    std::vector<uint32_t> dt;
+    std::vector<infw_dt_line> dte, dtl;  // decision-table entry and leaf lines
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -93,10 +92,13 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1
                    uint64_t dir24_budget = 4ull << 30);
 
 // Class-filtered GPU rule records of one 1200-B value (appended to rules) and
-// the per-class first-match decision tables (appended to dt).
-void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE],
-                       std::vector<uint32_t> &dt, uint64_t ddesc_out[INFW_DESC_STRIDE]);
+// the per-class first-match decision-table entry lines (leaf lines appended to leaves).
+int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE],
+                      infw_dt_line entry_out[INFW_NCLS], std::vector<infw_dt_line> &leaves);
 // Decision table of one class list (records {lo16, hi16, result32} in scan order).
-uint64_t build_decision_table(const std::vector<uint64_t> &recs, std::vector<uint32_t> &dt);
+int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry, std::vector<infw_dt_line> &leaves);
+// Entry (and leaf) lines of a step function: segment starts ascending from 0 and their results.
+int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
+                        std::vector<infw_dt_line> &leaves);
 
 }  // namespace infw

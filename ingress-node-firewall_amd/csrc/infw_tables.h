@@ -78,13 +78,25 @@ struct infw_v6_bucket {     // 64 B
 
 // First-match decision tables.  For one (rule list, packet class) the
 // first-match result as a function of the 16-bit packet value (dport, or
-// type << 8 | code) is a step function with S <= 2c + 1 segments.  It is stored
-// as a static 9-ary search tree over the segment starts (8 u16 keys per 16-B
-// node, key = start - 1 so that "key < v" <=> "start <= v"; pad 0xFFFF never
-// counts) followed by the S result words.  ddesc[list*8 + cls]:
-//   S == 0: no applicable rule (result 0); S == 1: bits 0..31 = the result;
-//   else bits 0..31 = offset in 16-B units, 32..47 = S, 48..55 = depth d.
-#define INFW_DT_FANOUT 9
+// type << 8 | code) is a step function with S <= 2c + 1 <= 201 segments.  It is
+// stored in 64-B lines (one L2 request each), so that a packet touches at most
+// two lines after the LPM answer:
+//   entry line   dte[list * INFW_NCLS + cls] — addressed directly from the LPM
+//                answer, no descriptor load in between;
+//   leaf form    (w[0] bit 31 clear; S <= 10): u16 keys in w[1..5] (key j =
+//                start of segment j+1 minus 1, so "key < v" <=> "start <= v";
+//                pad 0xFFFF never counts) and the results in w[6..15]; the
+//                result is w[6 + #keys below v];
+//   root form    (bit 31 set; S <= 310): 30 u16 group keys in w[1..15] select
+//                one of <= 31 leaf lines dtl[(w[0] & 0x7FFFFFFF) + #keys below v],
+//                each a leaf-form line over 10 consecutive segments.
+// No applicable rule is the all-pad leaf with result 0.
+#define INFW_DT_LEAF_SEGS 10u
+#define INFW_DT_ROOT_KEYS 30u
+#define INFW_DT_ROOT 0x80000000u
+struct infw_dt_line {       // 64 B
+    uint32_t w[16];
+};
 
 // Compressed short table (the <= /32 key space), per slot: l16[slot][2^16]
 // words indexed by address bits 0..15; a word is list+1 (0 = none) or, with
@@ -119,8 +131,8 @@ struct infw_dev_tables {
     uint64_t bmask;
     const uint64_t *desc;      // ballot mode: off | cnt << 32 into rules
     const uint64_t *rules;
-    const uint64_t *ddesc;     // decision mode (see above)
-    const uint32_t *dt;          // decision-table pool, 16-B units
+    const struct infw_dt_line *dte;  // decision mode: entry lines, n_lists * INFW_NCLS
+    const struct infw_dt_line *dtl;  // decision mode: leaf lines
     const uint8_t *levels;     // n_levels distinct long lengths, ascending
     uint32_t n_levels;
 };
@@ -204,23 +216,27 @@ INFW_TD uint32_t infw_count_lt(uint32_t w, uint32_t v) {  // keys (two u16) belo
     return (uint32_t)((w & 0xFFFFu) < v) + (uint32_t)((w >> 16) < v);
 }
 
-// First-match result of decision-table descriptor dd for value v.
+// Keys (u16 halves of words w[a..b)) below v.
+INFW_TD uint32_t infw_keys_below(const uint32_t *w, int a, int b, uint32_t v) {
+    uint32_t c = 0;
+    for (int k = a; k < b; k++) c += infw_count_lt(w[k], v);
+    return c;
+}
+
+// Result of a leaf-form line for v.
+INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
+    const uint32_t c = infw_keys_below(w, 1, 6, v);
+    uint32_t r = w[6];
+    for (uint32_t k = 1; k < INFW_DT_LEAF_SEGS; k++) r = c >= k ? w[6 + k] : r;
+    return r;
+}
+
+// First-match result of (list, cls) for value v (host walk; the kernel has its own loads).
 template <class T>
-INFW_TD uint32_t infw_dt_eval(const T &t, uint64_t dd, uint32_t v) {
-    const uint32_t S = (uint32_t)(dd >> 32) & 0xFFFFu;
-    if (S <= 1) return S ? (uint32_t)dd : 0u;
-    const uint32_t d = (uint32_t)(dd >> 48) & 0xFFu;
-    const uint32_t *base = reinterpret_cast<const uint32_t *>(t.dt) + 4ull * (uint32_t)dd;
-    uint32_t node = 0, lvl = 0, span = d == 1 ? 9u : d == 2 ? 81u : 729u;
-    for (uint32_t l = 0; l < d; l++) {
-        const uint32_t *k = base + 4ull * (lvl + node);
-        const uint32_t c = infw_count_lt(k[0], v) + infw_count_lt(k[1], v) + infw_count_lt(k[2], v) +
-                           infw_count_lt(k[3], v);
-        lvl += (S + span - 1) / span;  // nodes on level l
-        span /= 9u;
-        node = node * 9u + c;
-    }
-    return base[4ull * lvl + node];
+INFW_TD uint32_t infw_dt_eval(const T &t, uint32_t list, int cls, uint32_t v) {
+    const uint32_t *w = t.dte[(uint64_t)list * INFW_NCLS + cls].w;
+    if (w[0] & INFW_DT_ROOT) w = t.dtl[(w[0] & ~INFW_DT_ROOT) + infw_keys_below(w, 1, 16, v)].w;
+    return infw_dt_leaf(w, v);
 }
 
 // Table pointers are read through T so host and device share the walk.
@@ -262,6 +278,7 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 // exceeds the memory budget, then the compressed 16-8-8 form (~16 B per prefix).
 #define INFW_SHORT_DIR24 0u
 #define INFW_SHORT_COMPRESSED 1u
+#define INFW_SHORT_NONE 2u        // DIR-24-8 build without any <= /32 entry
 
 template <class T>
 INFW_TD uint32_t infw_dir24_lookup(const T &t, uint32_t slot, uint32_t a32) {
@@ -335,7 +352,8 @@ INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uin
 
 template <class T>
 INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
-    return t.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(t, slot, a32) : infw_dir_lookup(t, slot, a32);
+    if (t.short_mode == INFW_SHORT_DIR24) return infw_dir24_lookup(t, slot, a32);
+    return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }
 
 // list+1 of the longest matching entry, 0 if none.

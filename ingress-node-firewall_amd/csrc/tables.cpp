@@ -188,9 +188,46 @@ int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
 // keeping the lowest-index rule covering it (min-heap with lazy deletion),
 // merge equal neighbours, then lay the segment starts out as a 9-ary search
 // tree (infw_tables.h) followed by the results.
-uint64_t build_decision_table(const std::vector<uint64_t> &recs, std::vector<uint32_t> &dt) {
+// Lay one step function (segment starts ascending from 0, results) out as an
+// entry line and, above INFW_DT_LEAF_SEGS segments, leaf lines (infw_tables.h).
+static void fill_leaf(infw_dt_line &l, const uint32_t *starts, const uint32_t *res, uint32_t n) {
+    uint16_t key[2 * 5];
+    for (uint32_t j = 0; j < 10; j++) key[j] = j + 1 < n ? (uint16_t)(starts[j + 1] - 1) : (uint16_t)0xFFFF;
+    l.w[0] = n;
+    for (uint32_t k = 0; k < 5; k++) l.w[1 + k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
+    for (uint32_t j = 0; j < INFW_DT_LEAF_SEGS; j++) l.w[6 + j] = j < n ? res[j] : res[n - 1];
+}
+
+int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
+                        std::vector<infw_dt_line> &leaves) {
+    const uint32_t S = (uint32_t)starts.size();
+    memset(&entry, 0, sizeof(entry));
+    if (S <= INFW_DT_LEAF_SEGS) {
+        fill_leaf(entry, starts.data(), res.data(), S);
+        return 0;
+    }
+    const uint32_t G = (S + INFW_DT_LEAF_SEGS - 1) / INFW_DT_LEAF_SEGS;
+    if (G > INFW_DT_ROOT_KEYS + 1 || leaves.size() + G > INFW_DT_ROOT) return -ENOSPC;
+    entry.w[0] = INFW_DT_ROOT | (uint32_t)leaves.size();
+    uint16_t key[2 * 15];
+    for (uint32_t j = 0; j < INFW_DT_ROOT_KEYS; j++)
+        key[j] = j + 1 < G ? (uint16_t)(starts[(j + 1) * INFW_DT_LEAF_SEGS] - 1) : (uint16_t)0xFFFF;
+    for (uint32_t k = 0; k < 15; k++) entry.w[1 + k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
+    for (uint32_t g = 0; g < G; g++) {
+        infw_dt_line l;
+        const uint32_t a = g * INFW_DT_LEAF_SEGS, n = std::min(INFW_DT_LEAF_SEGS, S - a);
+        fill_leaf(l, starts.data() + a, res.data() + a, n);
+        leaves.push_back(l);
+    }
+    return 0;
+}
+
+int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry, std::vector<infw_dt_line> &leaves) {
     const size_t c = recs.size();
-    if (c == 0) return 0;
+    if (c == 0) {
+        const std::vector<uint32_t> z0{0}, r0{0};
+        return emit_decision_lines(z0, r0, entry, leaves);
+    }
     std::vector<std::pair<uint32_t, uint32_t>> ev;  // (position, rule index) starts
     std::vector<std::pair<uint32_t, uint32_t>> en;  // (position, rule index) ends (hi + 1)
     std::vector<uint32_t> pts{0};
@@ -224,37 +261,13 @@ uint64_t build_decision_table(const std::vector<uint64_t> &recs, std::vector<uin
             res.push_back(r);
         }
     }
-    const uint32_t S = (uint32_t)starts.size();
-    if (S == 1) return (uint64_t)res[0] | 1ull << 32;
-    uint32_t d = 1, span = 9;
-    while (span < S) {
-        d++;
-        span *= 9;
-    }
-    // offset in 16-B units
-    while (dt.size() & 3) dt.push_back(0);
-    const uint64_t off = dt.size() / 4;
-    if (off > 0xFFFFFFFFull) return ~0ull;
-    uint32_t sp = span;
-    for (uint32_t l = 0; l < d; l++) {
-        const uint32_t nodes = (S + sp - 1) / sp, child = sp / 9;
-        for (uint32_t k = 0; k < nodes; k++) {
-            uint16_t key[8];
-            for (uint32_t j = 0; j < 8; j++) {
-                uint64_t seg = ((uint64_t)k * 9 + j + 1) * child;
-                key[j] = seg < S ? (uint16_t)(starts[seg] - 1) : (uint16_t)0xFFFF;
-            }
-            for (uint32_t w = 0; w < 4; w++) dt.push_back((uint32_t)key[2 * w] | (uint32_t)key[2 * w + 1] << 16);
-        }
-        sp = child;
-    }
-    dt.insert(dt.end(), res.begin(), res.end());
-    return off | (uint64_t)S << 32 | (uint64_t)d << 48;
+    return emit_decision_lines(starts, res, entry, leaves);
 }
 
-void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
-                       uint64_t desc_out[INFW_DESC_STRIDE], std::vector<uint32_t> &dt,
-                       uint64_t ddesc_out[INFW_DESC_STRIDE]) {
+int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
+                      uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line entry_out[INFW_NCLS],
+                      std::vector<infw_dt_line> &leaves) {
+    int rc = 0;
     std::vector<uint64_t> per[INFW_NCLS];
     for (int i = 0; i < INFW_MAX_RULES_PER_TARGET; i++) {
         const uint8_t *r = val + 12 * i;
@@ -292,7 +305,7 @@ void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
         }
     }
     for (int c = 0; c < INFW_DESC_STRIDE; c++) {
-        ddesc_out[c] = c < INFW_NCLS ? build_decision_table(per[c], dt) : 0;
+        if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], entry_out[c], leaves);
         if (c >= INFW_NCLS || per[c].empty()) {
             desc_out[c] = 0;
             continue;
@@ -301,6 +314,7 @@ void compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
         rules.insert(rules.end(), per[c].begin(), per[c].end());
         desc_out[c] = off | (uint64_t)per[c].size() << 32;
     }
+    return rc;
 }
 
 // ------------------------------------------------------------------------
@@ -393,7 +407,9 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     }
     out.n_lists = (uint32_t)list_of_vid.size();
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
-    out.ddesc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
+    out.dte.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS, infw_dt_line{});
+    out.dtl.clear();
+    int dt_rc = 0;
     {
         std::vector<std::pair<uint32_t, uint32_t>> by_lid(list_of_vid.begin(), list_of_vid.end());
         std::sort(by_lid.begin(), by_lid.end(),
@@ -401,16 +417,17 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
                       return a.second < b.second;
                   });
         for (auto &p : by_lid)
-            compile_rule_list(m.pool.vals[p.first].data(), out.rules, &out.desc[(size_t)p.second * INFW_DESC_STRIDE],
-                              out.dt, &out.ddesc[(size_t)p.second * INFW_DESC_STRIDE]);
+            if (!dt_rc)
+                dt_rc = compile_rule_list(m.pool.vals[p.first].data(), out.rules,
+                                          &out.desc[(size_t)p.second * INFW_DESC_STRIDE], &out.dte[(size_t)p.second * INFW_NCLS],
+                                          out.dtl);
     }
-    for (uint64_t dd : out.ddesc)
-        if (dd == ~0ull) {
-            set_error("compile: decision-table pool exceeds 64 GiB");
-            return -ENOSPC;
-        }
+    if (dt_rc) {
+        set_error("compile: decision-table leaf pool exceeds 2^31 lines");
+        return -ENOSPC;
+    }
     if (out.rules.empty()) out.rules.push_back(0);
-    while (out.dt.size() < 4 || (out.dt.size() & 3)) out.dt.push_back(0);
+    if (out.dtl.empty()) out.dtl.push_back(infw_dt_line{});
 
     // --- split entries
     std::vector<ShortEnt> shorts;
@@ -528,7 +545,10 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             si = sj;
         }
     }
-    if (out.tbl24.empty()) out.tbl24.push_back(0);
+    if (out.tbl24.empty()) {  // no <= /32 entry on any interface: nothing to index
+        out.tbl24.push_back(0);
+        if (out.short_mode == INFW_SHORT_DIR24) out.short_mode = INFW_SHORT_NONE;
+    }
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
     if (out.nodes.empty()) out.nodes.push_back(infw_bnode{});
     if (out.vpool.empty()) out.vpool.push_back(0);
@@ -659,8 +679,8 @@ infw_dev_tables HostTables::view() const {
     t.bmask = btab.size() - 1;
     t.desc = desc.data();
     t.rules = rules.data();
-    t.ddesc = ddesc.data();
-    t.dt = dt.data();
+    t.dte = dte.data();
+    t.dtl = dtl.data();
     t.n_levels = (uint32_t)levels.size();
     t.levels = levels.data();
     return t;

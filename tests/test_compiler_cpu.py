@@ -5,6 +5,7 @@ Waldvogel overflow table + class-filtered rule lists; infw_debug_walk runs the
 kernel's lookup code over that image on the host.  These tests compare it with
 the oracle on the BASELINE workloads and on adversarial random tables.
 """
+import os
 import random
 import struct
 
@@ -185,3 +186,16 @@ def test_decision_tables_exhaustive_values():
             n = np.full(65536, 100, np.uint32)
             want, _, _, _ = m.classify_frames(hdr, n, n, np.full(65536, 9, np.uint32), nthreads=4)
             assert np.array_equal(got, want), (t, src, proto, np.nonzero(got != want)[0][:5])
+
+
+def test_host_sanitizer_walk():
+    """tools/asan_walk.cpp under AddressSanitizer/UBSan: the compiler and the shared
+    host/device walk over random tables in every short-table form (incl. a DIR-24-8
+    build with no <= /32 entry), decision tables checked against the serial scan."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "asan"], cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]

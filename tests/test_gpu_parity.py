@@ -252,3 +252,31 @@ def test_pack_frames_on_device():
     torch.cuda.synchronize()
     h2, c2, p2 = snapshots(fr)
     assert np.array_equal(out2.to_tuples(), W.pack_frames(h2, c2, p2, ifs))
+
+
+@pytest.mark.parametrize("short_table", ["dir24", "compressed"])
+def test_survey_probes_on_device(monkeypatch, short_table):
+    """Every probe of tests/golden/survey_probes.json (the reference's edge semantics:
+    truncation, family gating, unified key space, IPv4-mapped keys, tables with no
+    <= /32 entry ...) through the HIP kernel: verdicts, result words and counters."""
+    import goenc
+    from frames import snapshots
+    from test_golden import expected_stats, load, probe_frames
+    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
+    dev = torch.device("cuda", 0)
+    for case in load("survey_probes.json")["cases"]:
+        c = infw.Classifier(devices=[0])
+        for e in case["table"]:
+            c.update(infw.build_ebpf_key(e["key"]["ifindex"], e["key"]["cidr"]),
+                     infw.RulesValSt.from_buffer_copy(goenc.raw_value(e["rules"])))
+        c.commit()
+        frames, ifx = probe_frames(case)
+        hdr, cap, pl = snapshots(frames)
+        tuples = W.pack_frames(hdr, cap, pl, np.array(ifx, np.uint32))
+        n = tuples.shape[0]
+        res, ver = gpu_run(c, SoaBatch.from_tuples(tuples, dev), n)
+        for p, v, r in zip(case["packets"], ver, res):
+            assert v == p["expect"]["retval"], (case["name"], p, v, hex(r))
+            if "result" in p["expect"]:
+                assert r == p["expect"]["result"], (case["name"], p, hex(r))
+        assert np.array_equal(c.stats_read_all(), expected_stats(case, frames)), case["name"]

@@ -1,0 +1,99 @@
+// Host-only AddressSanitizer/UBSan run of the table compiler and of the shared
+// host/device walk (infw_tables.h) over random tables: every compiled form
+// (DIR-24-8, compressed 16-8-8, no short entries, IPv6 buckets and overflow
+// groups, decision-table entry/leaf lines) is indexed the way the kernel does.
+// Build + run: make asan
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+
+#include "../ingress-node-firewall_amd/csrc/infw_internal.h"
+
+namespace infw {
+void set_error(const std::string &s) { fprintf(stderr, "set_error: %s\n", s.c_str()); }
+}  // namespace infw
+using namespace infw;
+
+static uint64_t rs = 0x1234567;
+static uint32_t rnd() {
+    rs ^= rs << 13;
+    rs ^= rs >> 7;
+    rs ^= rs << 17;
+    return (uint32_t)(rs >> 11);
+}
+
+static void random_value(uint8_t *val, int n_rules) {
+    memset(val, 0, 1200);
+    for (int i = 0; i < n_rules; i++) {
+        uint8_t *r = val + 12 * (1 + rnd() % 99);
+        uint32_t id = 1 + rnd() % 5000;
+        memcpy(r, &id, 4);
+        const uint8_t protos[6] = {0, 6, 17, 132, 1, 58};
+        r[4] = protos[rnd() % 6];
+        uint16_t ps = (uint16_t)rnd(), pe = (rnd() & 1) ? 0 : (uint16_t)(ps + rnd() % 3000);
+        memcpy(r + 5, &ps, 2);
+        memcpy(r + 7, &pe, 2);
+        r[9] = (uint8_t)(rnd() % 4 ? 8 : rnd());
+        r[10] = (uint8_t)(rnd() % 3);
+        r[11] = (uint8_t)(1 + rnd() % 3);
+    }
+}
+
+static int run_case(int n_keys, int v4_share, int max_rules, int mode, int seed) {
+    rs = 0x9E3779B97F4A7C15ull * (uint64_t)(seed + 1);
+    PendingMap m;
+    m.max_entries = 1u << 20;
+    static uint8_t val[1200];
+    for (int i = 0; i < n_keys; i++) {
+        lpm_ip_key_st k;
+        memset(&k, 0, sizeof k);
+        k.ingress_ifindex = 1 + rnd() % 3;
+        const bool v4 = (int)(rnd() % 100) < v4_share;
+        const uint32_t len = v4 ? rnd() % 33 : (v4_share < 0 || rnd() % 4 == 0) ? 33 + rnd() % 96 : rnd() % 129;
+        k.prefixLen = len + 32;
+        for (int b = 0; b < 16; b++) k.ip_data[b] = (uint8_t)rnd();
+        if (rnd() % 4 == 0) k.ip_data[0] = k.ip_data[1] = k.ip_data[2] = k.ip_data[3] = 10;  // clustered groups
+        random_value(val, 1 + rnd() % max_rules);
+        m.update(&k, val, 0);
+    }
+    HostTables h;
+    int rc = compile_tables(m, h, mode, mode < 0 ? 0 : (4ull << 30));
+    if (rc) return rc;
+    const infw_dev_tables t = h.view();
+    uint64_t hits = 0;
+    for (int i = 0; i < 200000; i++) {
+        uint32_t sa[4] = {rnd(), rnd(), rnd(), rnd()};
+        if (rnd() % 2) sa[0] = 0x0A0A0A0Au;
+        const int pk = rnd() % 2 ? INFW_PK_V4 : INFW_PK_V6;
+        const uint32_t l1 = infw_lpm(t, pk, rnd() % 5, sa);
+        if (!l1) continue;
+        hits++;
+        const int cls = (int)(rnd() % INFW_NCLS);
+        const uint32_t v = rnd() & 0xFFFF;
+        const uint32_t a = infw_dt_eval(t, l1 - 1, cls, v);
+        const uint32_t b = infw_scan_serial(t, t.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls], v);
+        if (a != b) {
+            fprintf(stderr, "mismatch: list %u cls %d v %u: table %x scan %x\n", l1 - 1, cls, v, a, b);
+            return -1;
+        }
+    }
+    printf("keys %d v4%% %d rules<=%d mode %d: lists %u short_mode %u hits %llu\n", n_keys, v4_share, max_rules, mode,
+           h.n_lists, h.short_mode, (unsigned long long)hits);
+    return 0;
+}
+
+int main() {
+    int bad = 0;
+    const int modes[3] = {INFW_SHORT_DIR24, INFW_SHORT_COMPRESSED, -1};
+    for (int s = 0; s < 3; s++)
+        for (int mi = 0; mi < 3; mi++) {
+            bad |= run_case(2000, 50, 99, modes[mi], s) != 0;
+            bad |= run_case(300, 0, 10, modes[mi], s) != 0;   // IPv6 only (long entries only for some seeds)
+            bad |= run_case(50, 100, 3, modes[mi], s) != 0;
+            bad |= run_case(1, 0, 1, modes[mi], s) != 0;
+            bad |= run_case(100, -1, 20, modes[mi], s) != 0;  // long (/33../128) entries only
+        }
+    printf(bad ? "FAILED\n" : "ok\n");
+    return bad;
+}
