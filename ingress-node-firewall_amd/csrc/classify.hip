@@ -3,19 +3,20 @@
 //
 // A persistent grid of kBlock-thread workgroups strides over the batch one
 // tile (kBlock packets, one per lane) at a time.  Per tile:
-//   1. each lane loads one 32-B tuple (five coalesced streams), parses it
-//      (infw_parse) and walks the LPM (ifindex hash -> IPv6 long table ->
-//      DIR-24-8), then gathers the rule-list descriptor of its packet class;
-//   2. the wave resolves first-match cooperatively, one lane per rule: it takes
-//      the lanes that need a scan G at a time (s_ff1 over a ballot), issues the
-//      G packets' 64-rule chunk loads back to back (G loads in flight instead
-//      of one dependent round trip per packet), then for each packet tests
-//      lo <= v <= hi on all 64 lanes and __ballot/ffs picks the first match —
-//      the reference's in-order scan (kernel.c:222-258) in one wave step per
-//      64 rules;
-//   3. result words / verdicts are stored coalesced; allow/deny counters
-//      accumulate in LDS (u32 packets, u64 bytes per rule id) and are flushed
-//      with one u64 atomic per touched counter when the workgroup retires.
+//   1. each lane loads one 32-B tuple (five coalesced non-temporal streams; the
+//      next tile's tuple is in flight while this one walks the tables), parses
+//      it (infw_parse) and walks the LPM (ifindex map in LDS -> IPv6 /32-group
+//      bucket -> DIR-24-8);
+//   2. first match (default, G == 0): the LPM answer addresses the 64-B
+//      decision-table entry line of (list, class) directly; an entry with more
+//      than 10 segments selects one 64-B leaf line — at most two table lines per
+//      packet after the LPM (infw_tables.h).  G > 0 keeps the one-lane-per-rule
+//      ballot scan of the class list (the reference's in-order scan,
+//      kernel.c:222-258, one wave step per 64 rules, G packets in flight);
+//   3. result words / verdicts are stored coalesced; allow/deny counters are
+//      summed per wavefront for the leading counter slot, the rest go to LDS
+//      atomics (u32 packets, u64 bytes per rule id), flushed with one u64
+//      atomic per touched counter when the workgroup retires.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -1,0 +1,82 @@
+// Microbenchmark: random per-lane gathers on gfx950 — what one packet's table
+// touches cost.  Each lane issues `iters` independent lookups (index from a
+// counter hash), each reading W bytes (4, 8, 16, 32, 64) of one random
+// W-aligned record of a T-byte table.  Reports lookups/s and record bytes/s.
+//   hipcc --offload-arch=gfx950 -O3 tools/micro/gather.hip -o gather && ./gather
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+template <int W, bool kDep>
+__global__ __launch_bounds__(512, 8) void gather(const uint32_t *__restrict__ tab, uint32_t mask, int iters,
+                                                 uint32_t *__restrict__ out) {
+    const uint32_t tid = blockIdx.x * 512 + threadIdx.x;
+    uint32_t acc = 0, idx = mix(tid);
+    for (int it = 0; it < iters; it++) {
+        const uint32_t rec = (kDep ? mix(idx ^ acc) : mix(idx + it * 0x9E3779B9u)) & mask;
+        if (W == 4) {
+            acc += tab[rec];
+        } else if (W == 8) {
+            const uint2 v = reinterpret_cast<const uint2 *>(tab)[rec];
+            acc += v.x ^ v.y;
+        } else {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(tab) + (uint64_t)rec * (W / 16);
+#pragma unroll
+            for (int k = 0; k < W / 16; k++) {
+                const u32x4 v = p[k];
+                acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+            }
+        }
+    }
+    out[tid] = acc;
+}
+
+template <int W, bool kDep>
+void run(const uint32_t *tab, uint64_t tbytes, uint32_t *out, int grid, int iters, const char *name) {
+    const uint32_t mask = (uint32_t)(tbytes / W - 1);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    gather<W, kDep><<<grid, 512>>>(tab, mask, iters, out);
+    hipEventRecord(a);
+    const int reps = 5;
+    for (int r = 0; r < reps; r++) gather<W, kDep><<<grid, 512>>>(tab, mask, iters, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double lookups = (double)grid * 512 * iters * reps;
+    printf("{\"test\": \"%s\", \"W\": %d, \"dep\": %d, \"table_MiB\": %.1f, \"Glookups_s\": %.2f, \"rec_TBs\": %.2f, \"ns_per_lookup_per_CU\": %.3f}\n",
+           name, W, (int)kDep, tbytes / 1048576.0, lookups / (ms * 1e-3) / 1e9, lookups * W / (ms * 1e-3) / 1e12,
+           (ms * 1e6) / (lookups / 256.0));
+    fflush(stdout);
+}
+
+int main() {
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const int grid = cus * 4;
+    const uint64_t max_t = 1ull << 30;
+    uint32_t *tab, *out;
+    hipMalloc(&tab, max_t);
+    hipMemset(tab, 1, max_t);
+    hipMalloc(&out, (size_t)grid * 512 * 4);
+    const uint64_t sizes[] = {1ull << 20, 16ull << 20, 128ull << 20, 1ull << 30};
+    for (uint64_t t : sizes) {
+        run<4, false>(tab, t, out, grid, 64, "indep");
+        run<8, false>(tab, t, out, grid, 64, "indep");
+        run<16, false>(tab, t, out, grid, 64, "indep");
+        run<32, false>(tab, t, out, grid, 64, "indep");
+        run<64, false>(tab, t, out, grid, 64, "indep");
+        run<4, true>(tab, t, out, grid, 64, "dep");
+        run<64, true>(tab, t, out, grid, 64, "dep");
+    }
+    return 0;
+}
