@@ -275,6 +275,30 @@ int infw_stats_bind(infw_ctx *ctx, int dev, uint64_t *device_stats);
 int infw_stats_device_ptr(infw_ctx *ctx, int dev, uint64_t **device_stats);
 
 /* ------------------------------------------------------------------------ */
+/* Debug lookup capture — ingress_node_firewall_dbg_map (kernel.c:59-64,     */
+/* HASH of lpm_ip_key_st -> lpm_ip_key_st, 16384 entries) filled with        */
+/* bpf_map_update_elem(key, key, BPF_NOEXIST) for every lookup key while the */
+/* load-time constant debug_lookup != 0 (kernel.c:78, :214-216, :297-299;    */
+/* loader.go:72-83 sets it from ENABLE_EBPF_LPM_LOOKUP_DBG).                 */
+/* Key inserted: packets whose L4 header was extracted (not UNDEF), before   */
+/* the LPM: {prefixLen 64, ifindex, saddr, 12 zero bytes} for IPv4,          */
+/* {160, ifindex, saddr[16]} for IPv6.  Existing keys are left alone; once   */
+/* INFW_DBG_MAX_ENTRIES distinct keys are held, new keys are dropped.        */
+/* One set per device (like one map per node); reads return their union,    */
+/* capped at INFW_DBG_MAX_ENTRIES.  Keys are deduplicated on the device by a */
+/* 64-bit fingerprint of the 24-B key.                                       */
+/* ------------------------------------------------------------------------ */
+#define INFW_DBG_MAX_ENTRIES 16384
+/* debug_lookup rewrite at load (loader.go:72-83).  Non-zero allocates the   */
+/* per-device key sets on first use; 0 stops capturing (keys are kept).      */
+int infw_debug_lookup_set(infw_ctx *ctx, uint32_t debug_lookup);
+/* Map iteration of the dbg map: copies up to cap keys, *n = keys held.       */
+/* Waits for work queued on the devices.                                      */
+int infw_debug_keys_read(infw_ctx *ctx, struct lpm_ip_key_st *keys, uint32_t cap, uint32_t *n);
+/* Delete every key of the dbg map (all devices).                             */
+int infw_debug_keys_clear(infw_ctx *ctx);
+
+/* ------------------------------------------------------------------------ */
 /* Control-plane encoders — the Go helpers whose byte output is the contract */
 /* of the table map.  Pure host functions (no device needed).                */
 /* ------------------------------------------------------------------------ */

@@ -8,14 +8,17 @@
 
 #include <chrono>
 #include <memory>
+#include <array>
 #include <mutex>
+#include <set>
 
 #include "infw_internal.h"
 
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
-                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count);
+                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
+                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots);
 
 extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
                                        uint32_t cus, hipStream_t stream);
@@ -67,7 +70,13 @@ struct Device {
     uint64_t *stats_own = nullptr;
     uint64_t *stats = nullptr;
     std::shared_ptr<DeviceEpoch> epoch;
+    // debug lookup capture set (allocated when debug_lookup is first set)
+    uint64_t *dbg_fp = nullptr;
+    uint32_t *dbg_keys = nullptr;
+    uint32_t *dbg_count = nullptr;
 };
+
+constexpr uint32_t kDbgSlots = 2 * INFW_DBG_MAX_ENTRIES;
 
 }  // namespace infw
 
@@ -81,6 +90,7 @@ struct infw_ctx {
     std::mutex epoch_mu;  // guards devs[*].epoch swaps vs classify snapshots
     // launch shape of the classify kernel (infw_set_launch / INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU)
     int block = 512, group = 0, blocks_per_cu = 4;
+    uint32_t debug_lookup = 0;  // kernel.c:78
     uint64_t epoch_no = 0;
     uint64_t committed_gen = ~0ull;
     struct infw_table_info info{};
@@ -206,6 +216,9 @@ void infw_destroy(infw_ctx *ctx) {
         DeviceGuard g(d.ordinal);
         (void)hipDeviceSynchronize();
         if (d.stats_own) (void)hipFree(d.stats_own);
+        if (d.dbg_fp) (void)hipFree(d.dbg_fp);
+        if (d.dbg_keys) (void)hipFree(d.dbg_keys);
+        if (d.dbg_count) (void)hipFree(d.dbg_count);
     }
     delete ctx;
 }
@@ -372,10 +385,67 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
     const bool evs = ex && ex->events_count;
     int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.cus, ctx->block,
                                   ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream),
-                                  evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr);
+                                  evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr,
+                                  ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots);
     if (rc) {
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
+    }
+    return 0;
+}
+
+int infw_debug_lookup_set(infw_ctx *ctx, uint32_t debug_lookup) {
+    if (!ctx) return -EINVAL;
+    if (debug_lookup)
+        for (auto &d : ctx->devs) {
+            if (d.dbg_fp) continue;
+            DeviceGuard g(d.ordinal);
+            if (!g.ok) return -ENODEV;
+            HIP_OK(hipMalloc(&d.dbg_fp, kDbgSlots * sizeof(uint64_t)));
+            HIP_OK(hipMalloc(&d.dbg_keys, kDbgSlots * 24));
+            HIP_OK(hipMalloc(&d.dbg_count, sizeof(uint32_t)));
+            HIP_OK(hipMemset(d.dbg_fp, 0, kDbgSlots * sizeof(uint64_t)));
+            HIP_OK(hipMemset(d.dbg_count, 0, sizeof(uint32_t)));
+        }
+    ctx->debug_lookup = debug_lookup;
+    return 0;
+}
+
+int infw_debug_keys_read(infw_ctx *ctx, lpm_ip_key_st *keys, uint32_t cap, uint32_t *n) {
+    if (!ctx || !n || (cap && !keys)) return -EINVAL;
+    std::set<std::array<uint8_t, 24>> all;
+    std::vector<uint64_t> fp(kDbgSlots);
+    std::vector<uint8_t> kb((size_t)kDbgSlots * 24);
+    for (auto &d : ctx->devs) {
+        if (!d.dbg_fp) continue;
+        DeviceGuard g(d.ordinal);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(fp.data(), d.dbg_fp, fp.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(kb.data(), d.dbg_keys, kb.size(), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < kDbgSlots && all.size() < INFW_DBG_MAX_ENTRIES; i++)
+            if (fp[i]) {
+                std::array<uint8_t, 24> k;
+                memcpy(k.data(), &kb[(size_t)i * 24], 24);
+                all.insert(k);
+            }
+    }
+    uint32_t i = 0;
+    for (const auto &k : all) {
+        if (i < cap) memcpy(&keys[i], k.data(), 24);
+        i++;
+    }
+    *n = i;
+    return 0;
+}
+
+int infw_debug_keys_clear(infw_ctx *ctx) {
+    if (!ctx) return -EINVAL;
+    for (auto &d : ctx->devs) {
+        if (!d.dbg_fp) continue;
+        DeviceGuard g(d.ordinal);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemset(d.dbg_fp, 0, kDbgSlots * sizeof(uint64_t)));
+        HIP_OK(hipMemset(d.dbg_count, 0, sizeof(uint32_t)));
     }
     return 0;
 }

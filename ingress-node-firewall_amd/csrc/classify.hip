@@ -95,15 +95,69 @@ struct EventSink {
     unsigned long long *count;
 };
 
+// Debug lookup capture (kernel.c:214-216, :297-299): an open-addressed set of
+// 2 * INFW_DBG_MAX_ENTRIES slots, a 64-bit key fingerprint per slot (0 = free)
+// claimed by CAS, the 24-B key beside it, and the number of keys held.
+struct DebugSink {
+    unsigned long long *fp;
+    uint32_t *keys;      // 6 words per slot
+    unsigned int *count;
+    uint32_t mask;
+};
+
+struct Sideband {
+    EventSink ev;
+    DebugSink dbg;
+};
+
+__device__ __forceinline__ uint64_t dbg_fingerprint(const uint32_t k[6]) {
+    uint64_t h = 0x243F6A8885A308D3ull;
+    for (int j = 0; j < 6; j++) {
+        h = (h ^ k[j]) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+    }
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return h | 1;
+}
+
+// bpf_map_update_elem(&dbg_map, &key, &key, BPF_NOEXIST): present -> no-op, full -> dropped.
+// The CAS is the arbiter (global atomics are performed at the memory side, so all XCDs agree);
+// the plain probe reads may be stale only towards "free", which just sends a lane to the CAS.
+__device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6]) {
+    const uint64_t fp = dbg_fingerprint(k);
+    uint32_t i = (uint32_t)(fp >> 32) & d.mask;
+    for (uint32_t probe = 0; probe <= d.mask; probe++) {
+        const uint64_t cur = __hip_atomic_load(&d.fp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == fp) return;
+        if (cur == 0) {
+            if (atomicAdd(d.count, 1u) >= INFW_DBG_MAX_ENTRIES) {  // reserve room first
+                atomicSub(d.count, 1u);
+                return;
+            }
+            const uint64_t old = atomicCAS(&d.fp[i], 0ull, (unsigned long long)fp);
+            if (old == 0) {
+                uint32_t *dst = d.keys + 6ull * i;
+                for (int j = 0; j < 6; j++) dst[j] = k[j];
+                return;
+            }
+            atomicSub(d.count, 1u);
+            if (old == fp) return;
+        }
+        i = (i + 1) & d.mask;
+    }
+}
+
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kPrefetch = !(kAblate & 128)>
+          bool kDebug = false, bool kPrefetch = !(kAblate & 128)>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
-                                                          const EventSink ev) {
+                                                          const Sideband sb) {
+    const EventSink &ev = sb.ev;
     __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
     __shared__ unsigned long long s_by[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
@@ -166,6 +220,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         }
         if (pk >= INFW_PK_V4) {
             const uint32_t sw[4] = {sa.x, sa.y, sa.z, sa.w};
+            if (kDebug) {  // lookup key {prefixLen 64|160, ifindex, ip_data} (kernel.c:205-216, :292-299)
+                // a full set stays as it is: skip the probe once INFW_DBG_MAX_ENTRIES keys are held
+                if (__hip_atomic_load(sb.dbg.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < INFW_DBG_MAX_ENTRIES) {
+                    const bool v6 = pk == INFW_PK_V6;
+                    const uint32_t key[6] = {v6 ? 160u : 64u, ifx, sa.x, v6 ? sa.y : 0u, v6 ? sa.z : 0u, v6 ? sa.w : 0u};
+                    dbg_insert(sb.dbg, key);
+                }
+            }
             uint32_t l1 = 1;  // diagnostic 1: no LPM walk, every parsed packet uses list 0
             if (!(kAblate & 1)) {
                 // ifindex -> slot (LDS copy of the open-addressed map)
@@ -304,15 +366,16 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     }
 }
 
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6)>
+template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
+          bool kDebug = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
-            EventSink ev = EventSink{nullptr, 0, nullptr}) {
+            const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves>), dim3(g), dim3(kBlock), 0, stream, *T, *in, n,
-                       results, verdicts, st, ev);
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug>), dim3(g), dim3(kBlock), 0, stream,
+                       *T, *in, n, results, verdicts, st, sb);
 }
 
 }  // namespace
@@ -324,12 +387,17 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
-                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count) {
+                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
+                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots) {
     if (n == 0) return 0;
-    if (ev_count) {  // event stream: the default launch shape with the sideband compiled in
+    if (ev_count || dbg_fp) {  // sidebands: the default launch shape with them compiled in
         auto *stt = reinterpret_cast<unsigned long long *>(stats);
-        launch<512, 0, 0, true>((uint32_t)blocks_per_cu, cus, T, in, n, results, verdicts, stt, stream,
-                                EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)});
+        const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
+                          DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
+        const uint32_t bpc = (uint32_t)blocks_per_cu;
+        if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+        else if (ev_count) launch<512, 0, 0, true, 8, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+        else launch<512, 0, 0, false, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);

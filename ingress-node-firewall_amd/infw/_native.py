@@ -110,12 +110,15 @@ assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12
 assert C.sizeof(RulesValSt) == 1200 and C.sizeof(RuleStatisticsSt) == 32
 
 # Every symbol include/infw.h declares (checked by tests/test_abi_cpu.py).
+DBG_MAX_ENTRIES = 16384  # include/infw.h INFW_DBG_MAX_ENTRIES (kernel.c:63)
+
 ABI_SYMBOLS = [
     "infw_classify_ex", "infw_pack_frames", "infw_create", "infw_destroy", "infw_num_devices", "infw_table_update", "infw_table_update_batch",
     "infw_table_delete", "infw_table_get_next_key", "infw_table_lookup", "infw_table_count",
     "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
+    "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear",
 ]
 
 
@@ -165,6 +168,9 @@ _sig = {
     "infw_table_info": (C.c_int, [C.c_void_p, P(TableInfo)]),
     "infw_debug_walk": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "infw_set_launch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "infw_debug_lookup_set": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "infw_debug_keys_read": (C.c_int, [C.c_void_p, P(LpmIpKeySt), C.c_uint32, P(C.c_uint32)]),
+    "infw_debug_keys_clear": (C.c_int, [C.c_void_p]),
     "infw_last_error": (C.c_char_p, []),
     "infw_abi_version": (C.c_int, []),
 }

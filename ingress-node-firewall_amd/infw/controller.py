@@ -13,6 +13,8 @@ netlink, pkg/interfaces/interfaces.go:85-116 — out of scope here).
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Union
@@ -51,14 +53,32 @@ def make_rules_val(rules: Sequence[ProtocolRule]) -> RulesValSt:
     return val
 
 
+DEBUG_LOOKUP_ENV = "ENABLE_EBPF_LPM_LOOKUP_DBG"
+
+
+def go_atoi(s: str) -> int:
+    """strconv.Atoi: optional sign, decimal digits only, int64 range; ValueError like the Go error."""
+    t = s[1:] if s[:1] in "+-" else s
+    if not t or not t.isascii() or not t.isdigit():
+        raise ValueError(f'failed to convert "{s}" to integer: strconv.Atoi: parsing "{s}": invalid syntax')
+    v = int(s)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError(f'failed to convert "{s}" to integer: strconv.Atoi: parsing "{s}": value out of range')
+    return v
+
+
 class IngNodeFwController:
     """IngNodeFwController (loader.go:43-50) with the table map on the GPU."""
 
     def __init__(self, classifier: Classifier, if_indices: Callable[[str], List[int]],
-                 is_valid_interface: Callable[[str], bool] = lambda name: True):
+                 is_valid_interface: Callable[[str], bool] = lambda name: True, environ=None):
         self.c = classifier
         self.if_indices = if_indices
         self.is_valid_interface = is_valid_interface
+        # debug_lookup constant from ENABLE_EBPF_LPM_LOOKUP_DBG (loader.go:37-38, :72-83)
+        env = os.environ if environ is None else environ
+        if DEBUG_LOOKUP_ENV in env:
+            self.c.debug_lookup(go_atoi(env[DEBUG_LOOKUP_ENV]) & 0xFFFFFFFF)
 
     def make_ingress_fw_rules_map(self, cfg: IngressNodeFirewallRules, if_id: int):
         val = make_rules_val(cfg.rules)

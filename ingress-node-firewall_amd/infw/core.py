@@ -210,6 +210,21 @@ class Classifier:
     def stats_bind(self, dev: int, ptr: Optional[int]) -> None:
         check(N.lib.infw_stats_bind(self._ctx, dev, ptr or None), "stats_bind")
 
+    # -- debug lookup capture (ingress_node_firewall_dbg_map, kernel.c:59-64, :214-216, :297-299)
+    def debug_lookup(self, value: int) -> None:
+        """The debug_lookup load-time constant (loader.go:72-83): non-zero captures every lookup key."""
+        check(N.lib.infw_debug_lookup_set(self._ctx, int(value)), "debug_lookup_set")
+
+    def debug_keys(self) -> list:
+        """Keys held by the debug map (union over devices), as 24-byte lpm_ip_key_st images."""
+        arr = (LpmIpKeySt * N.DBG_MAX_ENTRIES)()
+        n = C.c_uint32()
+        check(N.lib.infw_debug_keys_read(self._ctx, arr, N.DBG_MAX_ENTRIES, C.byref(n)), "debug_keys_read")
+        return [bytes(arr[i]) for i in range(min(n.value, N.DBG_MAX_ENTRIES))]
+
+    def debug_keys_clear(self) -> None:
+        check(N.lib.infw_debug_keys_clear(self._ctx), "debug_keys_clear")
+
     def stats_device_ptr(self, dev: int = 0) -> int:
         p = C.c_void_p()
         check(N.lib.infw_stats_device_ptr(self._ctx, dev, C.byref(p)), "stats_device_ptr")

@@ -535,3 +535,31 @@ uint64_t orc_collect_events(const orc_map *m, const uint8_t *frames, const uint6
     }
     return ne;
 }
+
+/* Debug lookup keys (kernel.c:205-216, :291-299): the key each frame would insert
+ * into ingress_node_firewall_dbg_map when debug_lookup != 0 — formed after the L4
+ * extraction succeeded and before the LPM lookup — in packet order, duplicates
+ * included.  keys_out: n_max x 24 B lpm_ip_key_st images. */
+uint64_t orc_collect_lookup_keys(const uint8_t *frames, const uint64_t *offsets, const uint32_t *caplen,
+                                 const uint32_t *pkt_len, const uint32_t *ifindex, uint64_t n,
+                                 uint8_t *keys_out, uint64_t n_max) {
+    uint64_t nk = 0;
+    for (uint64_t i = 0; i < n && nk < n_max; i++) {
+        const uint8_t *data = frames + offsets[i];
+        uint32_t lin = caplen[i] < pkt_len[i] ? caplen[i] : pkt_len[i];
+        if (ETH_HLEN > lin) continue;                                     /* :423-426 */
+        uint16_t h_proto = (uint16_t)(data[12] << 8 | data[13]);
+        int v4 = h_proto == 0x0800;
+        if (!v4 && h_proto != 0x86DD) continue;                           /* :436-438 */
+        uint16_t dstPort = 0;
+        uint8_t icmpCode = 0, icmpType = 0, proto = 0;
+        if (ip_extract_l4info(data, lin, &proto, &dstPort, &icmpType, &icmpCode, v4) < 0) continue;
+        uint8_t *k = keys_out + 24 * nk++;
+        memset(k, 0, 24);                                                 /* memset(&key, 0, ...) */
+        wr_le32(k, v4 ? 64u : 160u);                                      /* :207 / :293 */
+        wr_le32(k + 4, ifindex[i]);
+        if (v4) memcpy(k + 8, data + ETH_HLEN + 12, 4);                    /* :208-211 */
+        else memcpy(k + 8, data + ETH_HLEN + 8, 16);                       /* :294 */
+    }
+    return nk;
+}

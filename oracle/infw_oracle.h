@@ -93,6 +93,11 @@ uint64_t orc_collect_events(const orc_map *m, const uint8_t *frames, const uint6
                             const uint32_t *ifindex, uint64_t n, struct orc_event *events,
                             uint64_t max_events);
 
+/* Debug lookup keys (24-B lpm_ip_key_st images) in packet order, duplicates included. */
+uint64_t orc_collect_lookup_keys(const uint8_t *frames, const uint64_t *offsets, const uint32_t *caplen,
+                                 const uint32_t *pkt_len, const uint32_t *ifindex, uint64_t n,
+                                 uint8_t *keys_out, uint64_t n_max);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,8 @@ _sig = {
                                          C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "orc_collect_events": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
+    "orc_collect_lookup_keys": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_uint64, C.c_void_p, C.c_uint64]),
 }
 for _n, (_r, _a) in _sig.items():
     getattr(_lib, _n).restype = _r
@@ -136,3 +138,30 @@ class OracleMap:
                                     ifx.ctypes.data, n, ev, m)
         return np.array([(e.pkt_index, e.ifId, e.ruleId, e.action, e.pktLength, e.captured) for e in ev[:k]],
                         dtype=np.uint64).reshape(-1, 6)
+
+
+DBG_MAX_ENTRIES = 16384  # ingress_node_firewall_dbg_map max_entries (kernel.c:63)
+
+
+def debug_map_after(hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifindex: np.ndarray,
+                    max_entries: int = DBG_MAX_ENTRIES):
+    """Contents of the dbg map after the frames ran in packet order on one CPU: BPF_NOEXIST
+    inserts (kernel.c:214-216, :297-299) into a HASH of max_entries — the first max_entries
+    distinct lookup keys, in first-seen order.  Also returns the number of distinct keys."""
+    n = hdr.shape[0]
+    h = np.ascontiguousarray(hdr, dtype=np.uint8)
+    w = h.shape[1] if n else 0
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(w)
+    cap = np.ascontiguousarray(caplen, np.uint32)
+    pl = np.ascontiguousarray(pkt_len, np.uint32)
+    ifx = np.ascontiguousarray(ifindex, np.uint32)
+    out = np.zeros((max(n, 1), 24), np.uint8)
+    k = _lib.orc_collect_lookup_keys(h.ctypes.data, offs.ctypes.data, cap.ctypes.data, pl.ctypes.data,
+                                     ifx.ctypes.data, n, out.ctypes.data, n)
+    seen = {}
+    for row in out[:k]:
+        b = row.tobytes()
+        if b not in seen:
+            seen[b] = None
+    keys = list(seen)
+    return keys[:max_entries], len(keys)

@@ -73,3 +73,18 @@ def test_statistics_sum_and_overflow_rule():
     assert add_uint64(0, 5) == (5, True)
     assert add_uint64(2**64 - 1, 1) == (0, False)
     assert add_uint64(2**63, 2**62) == (2**63 + 2**62, True)
+
+
+def test_debug_lookup_env_go_atoi():
+    """ENABLE_EBPF_LPM_LOOKUP_DBG -> debug_lookup constant (loader.go:72-83): strconv.Atoi, uint32 wrap."""
+    from infw.controller import IngNodeFwController, go_atoi
+    assert go_atoi("1") == 1 and go_atoi("+7") == 7 and go_atoi("-1") == -1 and go_atoi("007") == 7
+    for bad in ("", " 1", "1 ", "0x10", "1.0", "+", "٣", "9223372036854775808"):
+        with pytest.raises(ValueError):
+            go_atoi(bad)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    IngNodeFwController(c, lambda n: [1], environ={"ENABLE_EBPF_LPM_LOOKUP_DBG": "1"})
+    IngNodeFwController(c, lambda n: [1], environ={})
+    with pytest.raises(ValueError):
+        IngNodeFwController(c, lambda n: [1], environ={"ENABLE_EBPF_LPM_LOOKUP_DBG": "yes"})
+    assert c.debug_keys() == []   # host-only context: no device sets

@@ -179,3 +179,26 @@ def test_demo1_sample():
     for src, proto, port, act, res in cases:
         a, r, _ = m.run(frame(src, proto=proto, dport=port), 1)
         assert (a, r) == (act, res), (src, proto, port)
+
+
+def test_debug_lookup_keys_oracle():
+    """The dbg-map key of each probe packet (kernel.c:205-216, :291-299): only packets whose L4 header was
+    extracted insert; IPv4 keys are {64, ifindex, saddr, 12 zero bytes}, IPv6 keys {160, ifindex, saddr}."""
+    import struct
+    need = {6: 20, 17: 8, 132: 12, 1: 8, 58: 8}
+    for case in load("survey_probes.json")["cases"]:
+        frames, ifx = probe_frames(case)
+        hdr, cap, pl = snapshots(frames)
+        keys, _ = orc.debug_map_after(hdr, cap, pl, np.array(ifx, np.uint32))
+        want = []
+        for f, i in zip(frames, ifx):
+            et = f[12] << 8 | f[13] if len(f) >= 14 else None
+            if et == 0x0800 and len(f) > 23 and f[23] in need and len(f) >= 34 + need[f[23]]:
+                k = struct.pack("<II", 64, i) + f[26:30] + bytes(12)
+            elif et == 0x86DD and len(f) > 20 and f[20] in need and len(f) >= 54 + need[f[20]]:
+                k = struct.pack("<II", 160, i) + f[22:38]
+            else:
+                continue
+            if k not in want:
+                want.append(k)
+        assert keys == want, case["name"]

@@ -280,3 +280,60 @@ def test_survey_probes_on_device(monkeypatch, short_table):
             if "result" in p["expect"]:
                 assert r == p["expect"]["result"], (case["name"], p, hex(r))
         assert np.array_equal(c.stats_read_all(), expected_stats(case, frames)), case["name"]
+
+
+def test_debug_lookup_capture():
+    """§8f-4 debug lookup capture (kernel.c:59-64, :214-216, :297-299): with debug_lookup set, the set of
+    lookup keys equals the oracle's dbg map (first-seen NOEXIST inserts, <= 16384 keys); repeats leave it
+    unchanged; classification is unaffected; once full, exactly 16384 keys, all of them real lookup keys."""
+    import orc
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 8000
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 555, 0)
+    hdr, cap, pl, ifx = wl.frames(555, n)
+    want, n_distinct = orc.debug_map_after(hdr, cap, pl, ifx)
+    assert 1000 < n_distinct < orc.DBG_MAX_ENTRIES
+    assert clf.debug_keys() == []
+    clf.debug_lookup(1)
+    clf.stats_reset()
+    gres, gver = gpu_run(clf, batch, n)
+    got = clf.debug_keys()
+    assert len(got) == len(want) and set(got) == set(want)
+    ores, over, ostats, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=4)
+    assert np.array_equal(gres, ores) and np.array_equal(gver, over)
+    assert np.array_equal(clf.stats_read_all(), ostats)
+    gpu_run(clf, batch, n)                       # NOEXIST: the same keys again change nothing
+    assert sorted(clf.debug_keys()) == sorted(want)
+    # heavy duplication inside waves and across workgroups: 64 distinct packets, 1024 copies each
+    clf.debug_keys_clear()
+    assert clf.debug_keys() == []
+    tup = np.tile(W.pack_frames(hdr[:64], cap[:64], pl[:64], ifx[:64]), (1024, 1))
+    gpu_run(clf, SoaBatch.from_tuples(tup, dev), tup.shape[0])
+    want64, _ = orc.debug_map_after(hdr[:64], cap[:64], pl[:64], ifx[:64])
+    assert sorted(clf.debug_keys()) == sorted(want64)
+    # debug_lookup 0: nothing captured
+    clf.debug_keys_clear()
+    clf.debug_lookup(0)
+    gpu_run(clf, batch, n)
+    assert clf.debug_keys() == []
+    # more distinct keys than the map holds: exactly 16384 keys, each a real lookup key of the batch
+    clf.debug_lookup(1)
+    nb = 1 << 17
+    big = SoaBatch.empty(nb, dev)
+    wl.gen_device(big, 1 << 20, 0)
+    hb, cb, pb, ib = wl.frames(1 << 20, nb)
+    allk, nd = orc.debug_map_after(hb, cb, pb, ib, max_entries=nb)
+    assert nd > orc.DBG_MAX_ENTRIES
+    gres_b, _ = gpu_run(clf, big, nb)
+    got = clf.debug_keys()
+    assert len(got) == orc.DBG_MAX_ENTRIES == len(set(got))
+    assert set(got) <= set(allk)
+    gpu_run(clf, batch, n)                       # full: new keys are dropped, the set is unchanged
+    assert set(clf.debug_keys()) == set(got)
+    assert np.array_equal(gres_b, m.classify_frames(hb, cb, pb, ib, nthreads=8)[0])

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -59,7 +60,7 @@ void run(const uint32_t *tab, uint64_t tbytes, uint32_t *out, int grid, int iter
     fflush(stdout);
 }
 
-int main() {
+int main(int argc, char **argv) {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int grid = cus * 4;
@@ -68,6 +69,14 @@ int main() {
     hipMalloc(&tab, max_t);
     hipMemset(tab, 1, max_t);
     hipMalloc(&out, (size_t)grid * 512 * 4);
+    if (argc > 1) {  // one configuration (PMC calibration): W=4 or 64, table MiB
+        const int w = atoi(argv[1]);
+        const uint64_t t = (uint64_t)atoi(argv[2]) << 20;
+        if (w == 4) run<4, false>(tab, t, out, grid, 64, "indep");
+        else if (w == 16) run<16, false>(tab, t, out, grid, 64, "indep");
+        else run<64, false>(tab, t, out, grid, 64, "indep");
+        return 0;
+    }
     const uint64_t sizes[] = {1ull << 20, 16ull << 20, 128ull << 20, 1ull << 30};
     for (uint64_t t : sizes) {
         run<4, false>(tab, t, out, grid, 64, "indep");
