@@ -286,7 +286,9 @@ int infw_stats_device_ptr(infw_ctx *ctx, int dev, uint64_t **device_stats);
 /* INFW_DBG_MAX_ENTRIES distinct keys are held, new keys are dropped.        */
 /* One set per device (like one map per node); reads return their union,    */
 /* capped at INFW_DBG_MAX_ENTRIES.  Keys are deduplicated on the device by a */
-/* 64-bit fingerprint of the 24-B key.                                       */
+/* 64-bit fingerprint of the 24-B key.  Which keys fill the last places when */
+/* more arrive at once is decided by the device's atomic order (the          */
+/* reference's by the CPUs' order).                                          */
 /* ------------------------------------------------------------------------ */
 #define INFW_DBG_MAX_ENTRIES 16384
 /* debug_lookup rewrite at load (loader.go:72-83).  Non-zero allocates the   */

@@ -423,7 +423,7 @@ int infw_debug_keys_read(infw_ctx *ctx, lpm_ip_key_st *keys, uint32_t cap, uint3
         HIP_OK(hipMemcpy(fp.data(), d.dbg_fp, fp.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
         HIP_OK(hipMemcpy(kb.data(), d.dbg_keys, kb.size(), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < kDbgSlots && all.size() < INFW_DBG_MAX_ENTRIES; i++)
-            if (fp[i]) {
+            if (fp[i] & 1) {  // a key's fingerprint (0 = free, 2 = tombstone)
                 std::array<uint8_t, 24> k;
                 memcpy(k.data(), &kb[(size_t)i * 24], 24);
                 all.insert(k);

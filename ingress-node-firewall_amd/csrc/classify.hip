@@ -122,27 +122,27 @@ __device__ __forceinline__ uint64_t dbg_fingerprint(const uint32_t k[6]) {
 }
 
 // bpf_map_update_elem(&dbg_map, &key, &key, BPF_NOEXIST): present -> no-op, full -> dropped.
-// The CAS is the arbiter (global atomics are performed at the memory side, so all XCDs agree);
-// the plain probe reads may be stale only towards "free", which just sends a lane to the CAS.
+// Slots are claimed by CAS (global atomics are performed at the memory side, so all XCDs agree),
+// then counted; a claim that finds the set full turns its slot into a tombstone, which probes
+// step over like any other key, so no probe chain ever breaks.  A plain read first lets repeats of
+// a held key return without an atomic (it can only be stale towards "free" or "tombstoned").
+constexpr unsigned long long kDbgTomb = 2ull;  // fingerprints are odd
 __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6]) {
     const uint64_t fp = dbg_fingerprint(k);
     uint32_t i = (uint32_t)(fp >> 32) & d.mask;
     for (uint32_t probe = 0; probe <= d.mask; probe++) {
-        const uint64_t cur = __hip_atomic_load(&d.fp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == fp) return;
-        if (cur == 0) {
-            if (atomicAdd(d.count, 1u) >= INFW_DBG_MAX_ENTRIES) {  // reserve room first
-                atomicSub(d.count, 1u);
-                return;
-            }
-            const uint64_t old = atomicCAS(&d.fp[i], 0ull, (unsigned long long)fp);
-            if (old == 0) {
+        if (__hip_atomic_load(&d.fp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fp) return;
+        const uint64_t old = atomicCAS(&d.fp[i], 0ull, (unsigned long long)fp);
+        if (old == fp) return;  // held
+        if (old == 0) {         // claimed: count it, or give the slot up as a tombstone when full
+            if (atomicAdd(d.count, 1u) < INFW_DBG_MAX_ENTRIES) {
                 uint32_t *dst = d.keys + 6ull * i;
                 for (int j = 0; j < 6; j++) dst[j] = k[j];
-                return;
+            } else {
+                atomicSub(d.count, 1u);
+                atomicExch(&d.fp[i], kDbgTomb);
             }
-            atomicSub(d.count, 1u);
-            if (old == fp) return;
+            return;
         }
         i = (i + 1) & d.mask;
     }
