@@ -129,11 +129,22 @@ def main():
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
 
     traffic = None
+    line_model = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_packet", None)
             traffic = None if traffic is None else round(traffic * n)
+            # random-line model: the kernel's PMC L2 hits/misses per packet priced at the
+            # chip's measured random-lookup rates; frac = that bound / the measured kernel time
+            r = tj.get("line_rates")
+            if r and "l2_hits_per_packet" in tj:
+                h, m = tj["l2_hits_per_packet"], tj["l2_misses_per_packet"]
+                bound_ms = n * (h / (r["l2_hit_G_per_s"] * 1e9) + m / (r["l2_miss_G_per_s"] * 1e9)) * 1e3
+                line_model = {"l2_hits_per_packet": round(h, 3), "l2_misses_per_packet": round(m, 3),
+                              "hit_rate_G_per_s": r["l2_hit_G_per_s"], "miss_rate_G_per_s": r["l2_miss_G_per_s"],
+                              "bound_ms": round(bound_ms, 3), "frac": round(bound_ms / avg_kern_ms, 3),
+                              "counters_from": tj.get("tag")}
         except Exception:
             traffic = None
 
@@ -168,9 +179,10 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
-            "kernel": "classify_kernel<true,false>",
+            "kernel": "classify_kernel<512, 0>",
             "kernel_ms_avg": round(avg_kern_ms, 4),
             "algorithmic_bytes_per_packet": ALGO_BYTES_PER_PKT,
+            "random_line_model": line_model,
         },
         "cpu_baseline": None,
     }

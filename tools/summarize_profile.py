@@ -62,6 +62,13 @@ def main():
     if "TCC_HIT_sum" in avg:
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         out["l2_misses_per_packet"] = avg["TCC_MISS_sum"] / n
+        out["l2_hits_per_packet"] = avg["TCC_HIT_sum"] / n
+        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+        if os.path.exists(tp):  # the random-line model bench.py reports beside the HBM roofline
+            tj = json.load(open(tp))
+            tj["l2_hits_per_packet"] = out["l2_hits_per_packet"]
+            tj["l2_misses_per_packet"] = out["l2_misses_per_packet"]
+            json.dump(tj, open(tp, "w"), indent=1)
     if "SQ_LDS_BANK_CONFLICT" in avg:
         out["lds_bank_conflict_rate"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"])
     if "GRBM_GUI_ACTIVE" in avg and out["kernels"]:
