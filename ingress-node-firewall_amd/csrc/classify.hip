@@ -68,11 +68,21 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
         const uint32_t g = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
                            lt2(b[3], v) + lt2(c[0], v) + lt2(c[1], v) + lt2(c[2], v) + lt2(c[3], v) + lt2(d[0], v) +
                            lt2(d[1], v) + lt2(d[2], v) + lt2(d[3], v);
-        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & ~INFW_DT_ROOT) + g));
+        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g));
         a = l[0];
         b = l[1];
         c = l[2];
         d = l[3];
+    }
+    if (a[0] & INFW_DT_COMPACT) {  // 19 u16 keys in w[1..10], u8 result codes in w[11..15]
+        const uint32_t k = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
+                           lt2(b[3], v) + lt2(c[0], v) + lt2(c[1], v) + lt2(c[2], v);
+        uint32_t w = c[3];
+        w = k >= 4 ? d[0] : w;
+        w = k >= 8 ? d[1] : w;
+        w = k >= 12 ? d[2] : w;
+        w = k >= 16 ? d[3] : w;
+        return infw_dt_code_result(__builtin_amdgcn_ubfe(w, 8 * (k & 3u), 8));
     }
     const uint32_t k = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v);
     uint32_t r = b[2];

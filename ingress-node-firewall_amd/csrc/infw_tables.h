@@ -87,13 +87,23 @@ struct infw_v6_bucket {     // 64 B
 //                start of segment j+1 minus 1, so "key < v" <=> "start <= v";
 //                pad 0xFFFF never counts) and the results in w[6..15]; the
 //                result is w[6 + #keys below v];
-//   root form    (bit 31 set; S <= 310): 30 u16 group keys in w[1..15] select
-//                one of <= 31 leaf lines dtl[(w[0] & 0x7FFFFFFF) + #keys below v],
-//                each a leaf-form line over 10 consecutive segments.
+//   compact leaf (w[0] bit 30; S <= 20): used when every result of the step
+//                function is 0 or SET_ACTIONRULE_RESPONSE(1|2, ruleId 1..127) —
+//                everything makeIngressFwRulesMap writes (loader.go:429-515):
+//                u16 keys in w[1..10], one result code per segment in the bytes
+//                of w[11..15]; code 0 = no match, else ruleId = code >> 1 and
+//                action = 1 + (code & 1).  Twice the segments of a u32 leaf, so
+//                half the leaf lines (and half the L2 footprint);
+//   root form    (bit 31 set): 30 u16 group keys in w[1..15] select one of
+//                <= 31 leaf lines dtl[(w[0] & 0x3FFFFFFF) + #keys below v], each
+//                a leaf over 10 (u32) or 20 (compact) consecutive segments.
 // No applicable rule is the all-pad leaf with result 0.
 #define INFW_DT_LEAF_SEGS 10u
+#define INFW_DT_CLEAF_SEGS 20u
 #define INFW_DT_ROOT_KEYS 30u
 #define INFW_DT_ROOT 0x80000000u
+#define INFW_DT_COMPACT 0x40000000u
+#define INFW_DT_INDEX 0x3FFFFFFFu
 struct infw_dt_line {       // 64 B
     uint32_t w[16];
 };
@@ -223,8 +233,23 @@ INFW_TD uint32_t infw_keys_below(const uint32_t *w, int a, int b, uint32_t v) {
     return c;
 }
 
-// Result of a leaf-form line for v.
+// Result word of a compact-leaf code (0 = no match).
+INFW_TD uint32_t infw_dt_code_result(uint32_t code) {
+    return code ? ((code >> 1) << 8 | (1u + (code & 1u))) : 0u;
+}
+// Compact-leaf code of a result word, or 0x100 when it has none.
+INFW_TD uint32_t infw_dt_result_code(uint32_t r) {
+    if (r == 0) return 0;
+    const uint32_t a = r & 0xFFu, id = r >> 8;
+    return (a == 1u || a == 2u) && id >= 1u && id <= 127u ? (id << 1 | (a - 1u)) : 0x100u;
+}
+
+// Result of a leaf line (u32 or compact form) for v.
 INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
+    if (w[0] & INFW_DT_COMPACT) {
+        const uint32_t c = infw_keys_below(w, 1, 11, v);  // 0..19
+        return infw_dt_code_result((w[11 + (c >> 2)] >> (8 * (c & 3u))) & 0xFFu);
+    }
     const uint32_t c = infw_keys_below(w, 1, 6, v);
     uint32_t r = w[6];
     for (uint32_t k = 1; k < INFW_DT_LEAF_SEGS; k++) r = c >= k ? w[6 + k] : r;
@@ -235,7 +260,7 @@ INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
 template <class T>
 INFW_TD uint32_t infw_dt_eval(const T &t, uint32_t list, int cls, uint32_t v) {
     const uint32_t *w = t.dte[(uint64_t)list * INFW_NCLS + cls].w;
-    if (w[0] & INFW_DT_ROOT) w = t.dtl[(w[0] & ~INFW_DT_ROOT) + infw_keys_below(w, 1, 16, v)].w;
+    if (w[0] & INFW_DT_ROOT) w = t.dtl[(w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, v)].w;
     return infw_dt_leaf(w, v);
 }
 

@@ -3,6 +3,8 @@
 // layout described in infw_tables.h.
 #include <errno.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <numeric>
 #include <queue>
@@ -190,33 +192,57 @@ int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
 // tree (infw_tables.h) followed by the results.
 // Lay one step function (segment starts ascending from 0, results) out as an
 // entry line and, above INFW_DT_LEAF_SEGS segments, leaf lines (infw_tables.h).
-static void fill_leaf(infw_dt_line &l, const uint32_t *starts, const uint32_t *res, uint32_t n) {
-    uint16_t key[2 * 5];
-    for (uint32_t j = 0; j < 10; j++) key[j] = j + 1 < n ? (uint16_t)(starts[j + 1] - 1) : (uint16_t)0xFFFF;
-    l.w[0] = n;
-    for (uint32_t k = 0; k < 5; k++) l.w[1 + k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
-    for (uint32_t j = 0; j < INFW_DT_LEAF_SEGS; j++) l.w[6 + j] = j < n ? res[j] : res[n - 1];
+// Leaf over n <= segs consecutive segments: u16 keys (start of the next segment
+// minus 1, pad 0xFFFF) in the halves of w[1 ..], results after them.
+static void fill_leaf(infw_dt_line &l, const uint32_t *starts, const uint32_t *res, uint32_t n, bool compact) {
+    memset(&l, 0, sizeof(l));
+    const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS, kw = segs / 2;  // key words
+    for (uint32_t k = 0; k < kw; k++) {
+        uint32_t w = 0;
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t j = 2 * k + h;
+            w |= (uint32_t)(j + 1 < n ? (uint16_t)(starts[j + 1] - 1) : (uint16_t)0xFFFF) << (16 * h);
+        }
+        l.w[1 + k] = w;
+    }
+    if (compact) {
+        l.w[0] = INFW_DT_COMPACT | n;
+        for (uint32_t j = 0; j < segs; j++)
+            l.w[1 + kw + (j >> 2)] |= infw_dt_result_code(j < n ? res[j] : res[n - 1]) << (8 * (j & 3u));
+    } else {
+        l.w[0] = n;
+        for (uint32_t j = 0; j < segs; j++) l.w[1 + kw + j] = j < n ? res[j] : res[n - 1];
+    }
+}
+
+// INFW_DT_FORM=wide keeps every leaf in the u32 form (A/B measurements).
+static bool dt_compact_allowed() {
+    const char *e = getenv("INFW_DT_FORM");
+    return !(e && strcmp(e, "wide") == 0);
 }
 
 int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
                         std::vector<infw_dt_line> &leaves) {
     const uint32_t S = (uint32_t)starts.size();
+    bool compact = dt_compact_allowed();
+    for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
+    const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
     memset(&entry, 0, sizeof(entry));
-    if (S <= INFW_DT_LEAF_SEGS) {
-        fill_leaf(entry, starts.data(), res.data(), S);
+    if (S <= segs) {
+        fill_leaf(entry, starts.data(), res.data(), S, compact);
         return 0;
     }
-    const uint32_t G = (S + INFW_DT_LEAF_SEGS - 1) / INFW_DT_LEAF_SEGS;
-    if (G > INFW_DT_ROOT_KEYS + 1 || leaves.size() + G > INFW_DT_ROOT) return -ENOSPC;
+    const uint32_t G = (S + segs - 1) / segs;
+    if (G > INFW_DT_ROOT_KEYS + 1 || leaves.size() + G > INFW_DT_INDEX) return -ENOSPC;
     entry.w[0] = INFW_DT_ROOT | (uint32_t)leaves.size();
     uint16_t key[2 * 15];
     for (uint32_t j = 0; j < INFW_DT_ROOT_KEYS; j++)
-        key[j] = j + 1 < G ? (uint16_t)(starts[(j + 1) * INFW_DT_LEAF_SEGS] - 1) : (uint16_t)0xFFFF;
+        key[j] = j + 1 < G ? (uint16_t)(starts[(j + 1) * segs] - 1) : (uint16_t)0xFFFF;
     for (uint32_t k = 0; k < 15; k++) entry.w[1 + k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
     for (uint32_t g = 0; g < G; g++) {
         infw_dt_line l;
-        const uint32_t a = g * INFW_DT_LEAF_SEGS, n = std::min(INFW_DT_LEAF_SEGS, S - a);
-        fill_leaf(l, starts.data() + a, res.data() + a, n);
+        const uint32_t a = g * segs, n = std::min(segs, S - a);
+        fill_leaf(l, starts.data() + a, res.data() + a, n, compact);
         leaves.push_back(l);
     }
     return 0;

@@ -139,7 +139,7 @@ def test_update_delete_churn_matches_oracle():
 def test_decision_tables_exhaustive_values():
     """Every 16-bit packet value for every packet class of random 100-slot rule lists: the compiled
     first-match decision tables (and, inside infw_debug_walk, the serial class-list scan) equal the
-    oracle's scan of the raw rulesVal_st."""
+    oracle's scan of the raw rulesVal_st — compact (u8 result code) and u32 leaf forms alike."""
     rng = random.Random(3)
     import goenc
     from frames import frame, snapshots
@@ -153,9 +153,13 @@ def test_decision_tables_exhaustive_values():
             ps = rng.randrange(0, 65536)
             kind = rng.random()
             pe = 0 if kind < 0.4 else min(65535, ps + rng.randrange(1, 4000)) if kind < 0.9 else rng.randrange(0, 65536)
-            rules.append({"slot": slot, "ruleId": slot, "protocol": proto, "dstPortStart": ps, "dstPortEnd": pe,
+            # t < 4: what the control plane writes (ruleId = order, Allow/Deny) -> compact leaves;
+            # t = 4: rule ids above 127, t = 5: actions outside {1, 2} -> u32 leaves
+            rid = slot + (100000 if t == 4 else 0)
+            act = rng.choice([0, 1, 2, 3, 200]) if t == 5 else rng.choice([1, 2])
+            rules.append({"slot": slot, "ruleId": rid, "protocol": proto, "dstPortStart": ps, "dstPortEnd": pe,
                           "icmpType": rng.randrange(256), "icmpCode": rng.randrange(256),
-                          "action": rng.choice([1, 2])})
+                          "action": act})
         ents.append((goenc.build_key(9, f"10.{t}.0.0/16"), goenc.raw_value(rules)))
         ents.append((goenc.build_key(9, f"2001:db8:{t}::/48"), goenc.raw_value(rules)))
     c = infw.Classifier(flags=infw.F_HOST_ONLY)

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""In-process A/B of table-layout variants on one resident batch (cfg2 by default).
+
+Each variant is a set of environment settings read by the table compiler at
+commit time (e.g. INFW_DT_FORM=wide, INFW_SHORT_TABLE=compressed); every
+variant gets its own Classifier (own device tables) over the same packets.
+Variants are interleaved over several rounds; result words and per-rule
+counters must be identical across variants.  Prints one JSON line per variant.
+  python tools/ab_tables.py --variants "base;INFW_DT_FORM=wide" [--cfg 2] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ingress-node-firewall_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 27)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--variants", default="base;INFW_DT_FORM=wide")
+    args = ap.parse_args()
+    import torch
+    import infw
+    from infw import workloads as W
+    from infw.batch import SoaBatch
+    dev = torch.device("cuda", 0)
+    wl = W.Workload(args.cfg)
+    n = args.batch
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 0, 0)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    names = [v.strip() for v in args.variants.split(";")]
+    clfs = {}
+    for v in names:
+        env = dict(kv.split("=", 1) for kv in v.split(",") if "=" in kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        c = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+        wl.load_into(c)
+        c.commit()
+        for k, old in saved.items():
+            if old is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old
+        info = c.info()
+        print(f"[ab] {v}: {info['device_bytes'] / 2**20:.0f} MiB, compile {info['compile_ms']:.0f} ms",
+              file=sys.stderr, flush=True)
+        clfs[v] = c
+    ref = None
+    times = {v: [] for v in names}
+    s = torch.cuda.current_stream()
+    for r in range(args.rounds):
+        for v in names:
+            c = clfs[v]
+            c.stats_reset()
+            c.classify(batch, results=res)
+            torch.cuda.synchronize()
+            if r == 0:
+                got = (res.clone(), c.stats_read_all())
+                if ref is None:
+                    ref = got
+                else:
+                    assert torch.equal(got[0], ref[0]), f"variant {v}: result words differ"
+                    assert (got[1] == ref[1]).all(), f"variant {v}: counters differ"
+            for _ in range(args.iters):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                c.classify(batch, results=res)
+                b.record(s)
+                b.synchronize()
+                times[v].append(a.elapsed_time(b))
+    for v in names:
+        t = times[v]
+        print(json.dumps({"variant": v, "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
+                          "gpps": round(n / statistics.median(t) / 1e6, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
