@@ -12,7 +12,8 @@ OBJ      := $(PKG)/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
 EXTRA    ?=
 
-LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip $(SRC)/pack.hip
+LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip \
+            $(SRC)/pack.hip $(SRC)/patch.hip
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 
@@ -46,7 +47,7 @@ asm:
 asan:
 	@mkdir -p $(OBJ)
 	g++ -std=c++17 -g -O1 -fsanitize=address,undefined -fno-sanitize-recover=undefined -Iinclude \
-	    tools/asan_walk.cpp $(SRC)/tables.cpp $(SRC)/controlplane.cpp -o $(OBJ)/asan_walk
+	    tools/asan_walk.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp -o $(OBJ)/asan_walk
 	$(OBJ)/asan_walk
 
 clean:

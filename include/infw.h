@@ -159,8 +159,11 @@ typedef struct infw_ctx infw_ctx;
 /* no CPU classification path.                                                */
 #define INFW_F_HOST_ONLY 0x1u   /* control plane only: map API + compile, no    */
                                 /* device tables; infw_classify -> -ENODEV     */
-#define INFW_F_KEEP_HOST_IMAGE 0x2u /* keep the compiled host table image for  */
-                                    /* infw_debug_walk (tests)                 */
+#define INFW_F_KEEP_HOST_IMAGE 0x2u /* accepted for compatibility: the host    */
+                                    /* image is always kept (incremental       */
+                                    /* commits patch it; infw_debug_walk reads) */
+#define INFW_F_FULL_COMMIT 0x4u     /* every commit recompiles the whole epoch  */
+                                    /* (env INFW_FULL_COMMIT=1 does the same)   */
 int infw_create(infw_ctx **out, const int *hip_devices, int n_dev,
                 uint32_t max_entries, uint32_t flags);
 void infw_destroy(infw_ctx *ctx);
@@ -196,8 +199,15 @@ int infw_table_get_next_key(infw_ctx *ctx, const struct lpm_ip_key_st *key,
 int infw_table_lookup(infw_ctx *ctx, const struct lpm_ip_key_st *key,
                       struct rulesVal_st *val);
 int infw_table_count(infw_ctx *ctx, uint64_t *n_entries);
-/* End of IngressNodeFwRulesLoader (loader.go:189-193): compile the pending   */
-/* set into GPU tables and swap epochs; in-flight batches finish on the old.  */
+/* End of IngressNodeFwRulesLoader (loader.go:189-193): publish the pending   */
+/* set as the next epoch; in-flight batches finish on the old one.            */
+/* Incremental by default: only the keys edited since the   */
+/* last commit are turned into table bytes (DIR-24-8 words / tbl8 groups,     */
+/* IPv6 buckets, appended rule lists), copied into the device's spare image,  */
+/* which then becomes live — each device keeps two images, so a batch always  */
+/* reads exactly one epoch.  Layout changes (new ifindex, overflowed IPv6     */
+/* groups, > 1/4 of the keys edited, ...) fall back to a full compile;        */
+/* infw_table_info reports which one ran and why.                             */
 int infw_table_commit(infw_ctx *ctx);
 
 /* ------------------------------------------------------------------------ */
@@ -334,7 +344,16 @@ struct infw_table_info {
     double upload_ms;          /* H2D time of the last commit                 */
     uint64_t n_v6_groups;      /* (ifindex, /32) groups of IPv6 long prefixes */
     uint64_t n_v6_overflow;    /* groups with > 3 long prefixes (Waldvogel)   */
+    uint32_t commit_mode;      /* INFW_COMMIT_*: how the last commit ran      */
+    uint32_t pad0;
+    uint64_t patch_bytes;      /* bytes copied to the devices by it           */
+    uint64_t dead_lists;       /* compiled lists no entry references (GC'd by */
+                               /* the next full compile)                      */
+    char full_reason[48];      /* why the last full compile was needed        */
 };
+#define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
+#define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */
+#define INFW_COMMIT_REUPLOAD 2u    /* patched host image, re-uploaded (grew)     */
 int infw_table_info(infw_ctx *ctx, struct infw_table_info *info);
 /* Verification hook for tests/ only — never called by infw_classify: walks     */
 /* the last committed HOST table image (INFW_F_HOST_ONLY or                      */
@@ -346,7 +365,7 @@ int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t 
 /* Last error string of this thread (static storage).                          */
 const char *infw_last_error(void);
 /* ABI version (bumped on incompatible change).                                */
-#define INFW_ABI_VERSION 1
+#define INFW_ABI_VERSION 2
 int infw_abi_version(void);
 
 #ifdef __cplusplus

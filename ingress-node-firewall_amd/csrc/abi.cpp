@@ -11,6 +11,8 @@
 #include <array>
 #include <mutex>
 #include <set>
+#include <thread>
+#include <algorithm>
 
 #include "infw_internal.h"
 
@@ -19,6 +21,13 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
                                     infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
                                     uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots);
+
+extern "C" int infw_launch_scatter(const uint32_t *staging, const void *descs, uint32_t n, uint32_t cus,
+                                   hipStream_t stream);
+
+struct infw_patch_desc {  // patch.hip
+    uint64_t dst, src, nwords;
+};
 
 extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
                                        uint32_t cus, hipStream_t stream);
@@ -50,26 +59,34 @@ struct DeviceGuard {
     }
 };
 
-// One epoch's tables resident on one device.
+// One table image resident on one device.  Buffers are allocated with room to
+// grow (appended rule lists and tbl8 groups), so an incremental commit can
+// patch an image in place; `pending` holds the host ranges changed since the
+// image was last brought up to date.
 struct DeviceEpoch {
     int ordinal = -1;
-    std::vector<void *> allocs;
+    void *buf[TB_COUNT] = {};
+    size_t cap[TB_COUNT] = {};
     infw_dev_tables view;
     uint64_t bytes = 0;
+    std::vector<DirtyRange> pending;
     ~DeviceEpoch() {
         if (ordinal < 0) return;
         DeviceGuard g(ordinal);
-        (void)hipDeviceSynchronize();  // batches launched on this epoch have finished
-        for (void *p : allocs) (void)hipFree(p);
+        (void)hipDeviceSynchronize();  // batches launched on this image have finished
+        for (void *p : buf)
+            if (p) (void)hipFree(p);
     }
 };
 
+// Two images per device: `epoch` is live (new batches read it), `spare` holds
+// the previous epoch and is patched up to the next one while `epoch` serves.
 struct Device {
     int ordinal = 0;
     uint32_t cus = 256;
     uint64_t *stats_own = nullptr;
     uint64_t *stats = nullptr;
-    std::shared_ptr<DeviceEpoch> epoch;
+    std::shared_ptr<DeviceEpoch> epoch, spare;
     // debug lookup capture set (allocated when debug_lookup is first set)
     uint64_t *dbg_fp = nullptr;
     uint32_t *dbg_keys = nullptr;
@@ -86,7 +103,8 @@ struct infw_ctx {
     std::vector<Device> devs;
     uint32_t flags = 0;
     PendingMap map;
-    std::unique_ptr<HostTables> host_image;  // INFW_F_HOST_ONLY / INFW_F_KEEP_HOST_IMAGE
+    std::unique_ptr<HostTables> host_image;  // the committed image (patched by incremental commits)
+    IncState inc;
     std::mutex epoch_mu;  // guards devs[*].epoch swaps vs classify snapshots
     // launch shape of the classify kernel (infw_set_launch / INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU)
     int block = 512, group = 0, blocks_per_cu = 4;
@@ -96,18 +114,7 @@ struct infw_ctx {
     struct infw_table_info info{};
 };
 
-template <class T>
-static int upload(DeviceEpoch &ep, const std::vector<T> &v, const T **dst) {
-    void *p = nullptr;
-    size_t bytes = v.size() * sizeof(T);
-    if (bytes == 0) bytes = sizeof(T);
-    HIP_OK(hipMalloc(&p, bytes));
-    ep.allocs.push_back(p);
-    if (!v.empty()) HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    ep.bytes += bytes;
-    *dst = static_cast<const T *>(p);
-    return 0;
-}
+static bool growable(int b) { return b == TB_TBL8 || b == TB_DESC || b == TB_RULES || b == TB_DTE || b == TB_DTL; }
 
 static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {
     DeviceGuard g(ordinal);
@@ -117,17 +124,33 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
     }
     auto ep = std::make_shared<DeviceEpoch>();
     ep->ordinal = ordinal;
+    for (int b = 0; b < TB_COUNT; b++) {
+        const void *p;
+        size_t bytes;
+        host_buffer(h, b, &p, &bytes);
+        size_t cap = bytes < 64 ? 64 : bytes;
+        if (growable(b)) cap += std::max<size_t>(bytes / 4, 256u << 10);
+        HIP_OK(hipMalloc(&ep->buf[b], cap));
+        ep->cap[b] = cap;
+        ep->bytes += cap;
+        if (bytes) HIP_OK(hipMemcpy(ep->buf[b], p, bytes, hipMemcpyHostToDevice));
+    }
     infw_dev_tables &t = ep->view;
     memset(&t, 0, sizeof(t));
-    int rc = 0;
-    if ((rc = upload(*ep, h.if_keys, &t.if_keys)) || (rc = upload(*ep, h.if_slot, &t.if_slot)) ||
-        (rc = upload(*ep, h.l16, &t.l16)) || (rc = upload(*ep, h.nodes, &t.nodes)) ||
-        (rc = upload(*ep, h.vpool, &t.vpool)) || (rc = upload(*ep, h.tbl24, &t.tbl24)) ||
-        (rc = upload(*ep, h.tbl8, &t.tbl8)) ||
-        (rc = upload(*ep, h.ltab, &t.ltab)) || (rc = upload(*ep, h.btab, &t.btab)) || (rc = upload(*ep, h.desc, &t.desc)) ||
-        (rc = upload(*ep, h.rules, &t.rules)) ||
-        (rc = upload(*ep, h.dte, &t.dte)) || (rc = upload(*ep, h.dtl, &t.dtl)) || (rc = upload(*ep, h.levels, &t.levels)))
-        return rc;
+    t.if_keys = static_cast<const uint32_t *>(ep->buf[TB_IFK]);
+    t.if_slot = static_cast<const uint32_t *>(ep->buf[TB_IFS]);
+    t.l16 = static_cast<const uint32_t *>(ep->buf[TB_L16]);
+    t.nodes = static_cast<const infw_bnode *>(ep->buf[TB_NODES]);
+    t.vpool = static_cast<const uint32_t *>(ep->buf[TB_VPOOL]);
+    t.tbl24 = static_cast<const uint32_t *>(ep->buf[TB_TBL24]);
+    t.tbl8 = static_cast<const uint32_t *>(ep->buf[TB_TBL8]);
+    t.ltab = static_cast<const infw_long_entry *>(ep->buf[TB_LTAB]);
+    t.btab = static_cast<const infw_v6_bucket *>(ep->buf[TB_BTAB]);
+    t.desc = static_cast<const uint64_t *>(ep->buf[TB_DESC]);
+    t.rules = static_cast<const uint64_t *>(ep->buf[TB_RULES]);
+    t.dte = static_cast<const infw_dt_line *>(ep->buf[TB_DTE]);
+    t.dtl = static_cast<const infw_dt_line *>(ep->buf[TB_DTL]);
+    t.levels = static_cast<const uint8_t *>(ep->buf[TB_LEVELS]);
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;
@@ -135,6 +158,73 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
     t.short_mode = h.short_mode;
     t.n_levels = (uint32_t)h.levels.size();
     out = ep;
+    return 0;
+}
+
+static bool image_fits(const DeviceEpoch &ep, const HostTables &h) {
+    for (int b = 0; b < TB_COUNT; b++) {
+        const void *p;
+        size_t bytes;
+        host_buffer(h, b, &p, &bytes);
+        if (bytes > ep.cap[b]) return false;
+    }
+    return true;
+}
+
+// Copy ep.pending (merged) from the host image into the device image: small
+// sets range by range, larger ones as one staging upload + one scatter launch.
+static int flush_pending(DeviceEpoch &ep, const HostTables &h, uint32_t cus, uint64_t *bytes_out) {
+    std::vector<DirtyRange> &r = ep.pending;
+    std::sort(r.begin(), r.end(), [](const DirtyRange &a, const DirtyRange &b) {
+        return a.buf != b.buf ? a.buf < b.buf : a.off < b.off;
+    });
+    std::vector<DirtyRange> m;
+    for (const DirtyRange &x : r) {
+        if (!m.empty() && m.back().buf == x.buf && x.off <= m.back().off + m.back().len + 64) {
+            m.back().len = std::max(m.back().off + m.back().len, x.off + x.len) - m.back().off;
+        } else {
+            m.push_back(x);
+        }
+    }
+    r.clear();
+    DeviceGuard g(ep.ordinal);
+    uint64_t total = 0;
+    std::vector<uint32_t> staging;
+    std::vector<infw_patch_desc> descs;
+    for (const DirtyRange &x : m) {
+        const void *p;
+        size_t bytes;
+        host_buffer(h, (int)x.buf, &p, &bytes);
+        const uint64_t len = std::min<uint64_t>(x.len, bytes > x.off ? bytes - x.off : 0);
+        if (!len) continue;
+        total += len;
+        const uint8_t *src = static_cast<const uint8_t *>(p) + x.off;
+        uint8_t *dst = static_cast<uint8_t *>(ep.buf[x.buf]) + x.off;
+        if (m.size() <= 16) {
+            HIP_OK(hipMemcpy(dst, src, len, hipMemcpyHostToDevice));
+            continue;
+        }
+        descs.push_back(infw_patch_desc{(uint64_t)(uintptr_t)dst, (uint64_t)staging.size(), len / 4});
+        staging.insert(staging.end(), reinterpret_cast<const uint32_t *>(src),
+                       reinterpret_cast<const uint32_t *>(src) + len / 4);
+    }
+    if (!descs.empty()) {
+        void *ds = nullptr, *dd = nullptr;
+        HIP_OK(hipMalloc(&ds, staging.size() * 4));
+        HIP_OK(hipMalloc(&dd, descs.size() * sizeof(infw_patch_desc)));
+        int rc = 0;
+        if (hipMemcpy(ds, staging.data(), staging.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dd, descs.data(), descs.size() * sizeof(infw_patch_desc), hipMemcpyHostToDevice) != hipSuccess ||
+            infw_launch_scatter(static_cast<const uint32_t *>(ds), dd, (uint32_t)descs.size(), cus, nullptr) ||
+            hipDeviceSynchronize() != hipSuccess) {
+            set_error(std::string("table patch upload failed: ") + hipGetErrorString(hipGetLastError()));
+            rc = -EIO;
+        }
+        (void)hipFree(ds);
+        (void)hipFree(dd);
+        if (rc) return rc;
+    }
+    if (bytes_out) *bytes_out += total;
     return 0;
 }
 
@@ -268,28 +358,87 @@ int infw_table_count(infw_ctx *ctx, uint64_t *n) {
 int infw_table_commit(infw_ctx *ctx) {
     if (!ctx) return -EINVAL;
     auto t0 = std::chrono::steady_clock::now();
-    HostTables h;
-    int mode = -1;
-    if (const char *e = getenv("INFW_SHORT_TABLE")) mode = strcmp(e, "compressed") == 0 ? 1 : strcmp(e, "dir24") == 0 ? 0 : -1;
-    int rc = compile_tables(ctx->map, h, mode);
-    if (rc) return rc;
-    auto t1 = std::chrono::steady_clock::now();
-    std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size());
-    for (size_t i = 0; i < ctx->devs.size(); i++) {
-        rc = upload_epoch(h, ctx->devs[i].ordinal, eps[i]);
-        if (rc) return rc;  // nothing swapped: the previous epoch stays live
+    std::vector<DirtyRange> ranges;
+    std::string why;
+    int rc = 1;
+    const char *fe = getenv("INFW_FULL_COMMIT");
+    const bool force_full = (ctx->flags & INFW_F_FULL_COMMIT) || (fe && atoi(fe) != 0);
+    if (ctx->host_image && !force_full) rc = patch_tables(ctx->map, *ctx->host_image, ctx->inc, ranges, &why);
+    if (rc < 0) rc = 1;  // the patch gave up half-way (image marked invalid): recompile
+    uint32_t mode = INFW_COMMIT_INCREMENTAL;
+    uint64_t patched = 0;
+    auto t1 = t0;
+    if (rc == 1) {
+        mode = INFW_COMMIT_FULL;
+        std::unique_ptr<HostTables> h(new HostTables());
+        int smode = -1;
+        if (const char *e = getenv("INFW_SHORT_TABLE")) smode = strcmp(e, "compressed") == 0 ? 1 : strcmp(e, "dir24") == 0 ? 0 : -1;
+        IncState inc;
+        rc = compile_tables(ctx->map, *h, smode, 4ull << 30, &inc);
+        if (rc) return rc;  // the previous epoch stays live
+        t1 = std::chrono::steady_clock::now();
+        std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size());
+        for (size_t i = 0; i < ctx->devs.size(); i++) {
+            rc = upload_epoch(*h, ctx->devs[i].ordinal, eps[i]);
+            if (rc) return rc;  // nothing swapped: the previous epoch stays live
+        }
+        std::vector<std::shared_ptr<DeviceEpoch>> old;
+        {
+            std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+            for (size_t i = 0; i < ctx->devs.size(); i++) {
+                old.push_back(ctx->devs[i].epoch);
+                old.push_back(ctx->devs[i].spare);
+                ctx->devs[i].epoch = eps[i];
+                ctx->devs[i].spare.reset();
+            }
+        }
+        old.clear();  // waits for batches still running on the old images, then frees them
+        ctx->host_image = std::move(h);
+        ctx->inc = std::move(inc);
+        for (auto &e : eps) patched += e->bytes;
+    } else {
+        t1 = std::chrono::steady_clock::now();
+        const HostTables &h = *ctx->host_image;
+        for (auto &d : ctx->devs) {
+            std::shared_ptr<DeviceEpoch> next;
+            if (d.spare && image_fits(*d.spare, h)) {
+                // batches that took the spare while it was live have launched and finished
+                while (d.spare.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+                {
+                    DeviceGuard g(d.ordinal);
+                    HIP_OK(hipDeviceSynchronize());
+                }
+                next = d.spare;
+                next->pending.insert(next->pending.end(), ranges.begin(), ranges.end());
+                rc = flush_pending(*next, h, d.cus, &patched);
+                if (rc) {
+                    std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+                    d.spare.reset();  // half-patched: never used again
+                    return rc;
+                }
+            } else {
+                rc = upload_epoch(h, d.ordinal, next);  // no spare yet, or it outgrew its buffers
+                if (rc) return rc;
+                if (d.spare) mode = INFW_COMMIT_REUPLOAD;
+                patched += next->bytes;
+            }
+            std::shared_ptr<DeviceEpoch> prev;
+            {
+                std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+                prev = d.epoch;
+                d.epoch = next;
+                d.spare.reset();
+                if (prev && image_fits(*prev, h)) {
+                    prev->pending.insert(prev->pending.end(), ranges.begin(), ranges.end());
+                    d.spare = prev;
+                }
+            }
+        }
     }
     auto t2 = std::chrono::steady_clock::now();
-    std::vector<std::shared_ptr<DeviceEpoch>> old(ctx->devs.size());
-    {
-        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
-        for (size_t i = 0; i < ctx->devs.size(); i++) {
-            old[i] = ctx->devs[i].epoch;
-            ctx->devs[i].epoch = eps[i];
-        }
-        ctx->epoch_no++;
-    }
-    old.clear();  // waits for batches still running on the old tables, then frees them
+    ctx->map.dirty.clear();
+    ctx->epoch_no++;
+    const HostTables &h = *ctx->host_image;
     struct infw_table_info &in = ctx->info;
     in.epoch = ctx->epoch_no;
     in.n_entries = h.n_entries;
@@ -299,21 +448,24 @@ int infw_table_commit(infw_ctx *ctx) {
     in.n_tbl8_groups = h.n_tbl8_groups;
     in.n_long_levels = (uint32_t)h.levels.size();
     in.n_long_entries = h.n_long_entries;
-    in.device_bytes = eps.empty() ? 0 : eps[0]->bytes;
+    in.device_bytes = ctx->devs.empty() || !ctx->devs[0].epoch ? 0 : ctx->devs[0].epoch->bytes;
     in.compile_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     in.n_v6_groups = h.n_buckets;
     in.n_v6_overflow = h.n_overflow_groups;
+    in.commit_mode = mode;
+    in.patch_bytes = patched;
+    in.dead_lists = ctx->inc.dead_lists;
+    memset(in.full_reason, 0, sizeof(in.full_reason));
+    if (mode == INFW_COMMIT_FULL) strncpy(in.full_reason, force_full ? "forced" : why.c_str(), sizeof(in.full_reason) - 1);
     ctx->committed_gen = ctx->map.generation;
-    if (ctx->flags & (INFW_F_HOST_ONLY | INFW_F_KEEP_HOST_IMAGE))
-        ctx->host_image.reset(new HostTables(std::move(h)));
     return 0;
 }
 
 int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t *out) {
     if (!ctx || (n && (!tuples || !out))) return -EINVAL;
     if (!ctx->host_image) {
-        set_error("debug_walk: no host table image (create with INFW_F_HOST_ONLY or INFW_F_KEEP_HOST_IMAGE)");
+        set_error("debug_walk: no committed table image");
         return -ENODATA;
     }
     const infw_dev_tables t = ctx->host_image->view();

@@ -1,0 +1,295 @@
+// incremental.cpp — patch the compiled table image with the keys edited since
+// the last commit, instead of recompiling the whole epoch.
+//
+// The reference updates its LPM trie one key at a time (addOrUpdateRules,
+// loader.go:200-208; purgeKeys, :633-649).  Here a commit turns the dirty keys
+// into the smallest set of changed table bytes:
+//   <= /32 entries   the DIR-24-8 words their prefix covers are recomputed
+//                    (longest entry <= /24 per tbl24 word, <= /32 per tbl8
+//                    entry); a /25../32 entry under a plain word gets a tbl8
+//                    group (appended; groups are never freed);
+//   IPv6 /33../128   the (slot, /32) group's 64-B bucket is rewritten (or
+//                    inserted into a free probe position);
+//   new rule values  their rule list is compiled and appended (decision lines,
+//                    class records) — lists are only appended, never moved.
+// Everything that would change the layout — a new ifindex, the compressed
+// short table, a group crossing 3 records (the Waldvogel overflow table), the
+// first long prefix, a bucket table past half load, too many edits, or half of
+// the lists unreferenced — is left to a full compile.  Decisions are made
+// before anything is modified, so "needs a full compile" leaves the image intact.
+#include <errno.h>
+
+#include <algorithm>
+
+#include "infw_internal.h"
+
+namespace infw {
+
+namespace {
+
+inline uint32_t rd_le32(const uint8_t *p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+struct Edit {
+    const NodeKey *key;
+    const NodeVal *now;  // nullptr: absent after the edits
+    int64_t was;         // committed value id, or PendingMap::kAbsent
+    uint32_t slot, P;    // address bits
+    uint32_t a32;        // address bits 0..31 (masked)
+    uint64_t hi, lo;     // full address (masked), big-endian halves
+};
+
+// 20-byte LPM key data {ifindex LE, address bits 0..31 BE, zeros}.
+inline void short_md(uint8_t md[20], const uint8_t ifx_le[4], uint32_t a32) {
+    memset(md, 0, 20);
+    memcpy(md, ifx_le, 4);
+    md[4] = (uint8_t)(a32 >> 24);
+    md[5] = (uint8_t)(a32 >> 16);
+    md[6] = (uint8_t)(a32 >> 8);
+    md[7] = (uint8_t)a32;
+}
+
+void mark(std::vector<DirtyRange> &r, int buf, uint64_t off, uint64_t len) {
+    if (len) r.push_back(DirtyRange{(uint32_t)buf, off, len});
+}
+
+}  // namespace
+
+int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
+                 std::string *why) {
+    auto full = [&](const char *reason) {
+        if (why) *why = reason;
+        return 1;
+    };
+    if (!inc.valid) return full("no compiled image to patch");
+    const size_t n_edits = m.dirty.size();
+    if (n_edits == 0) return 0;
+    if (n_edits > std::max<size_t>(65536, m.nodes.size() / 4)) return full("too many edits");
+
+    // ---- pass 1: classify the edits and check that the layout survives them
+    std::vector<Edit> edits;
+    edits.reserve(n_edits);
+    uint64_t short_words = 0;
+    bool any_short = false;
+    for (const auto &kv : m.dirty) {
+        Edit e;
+        e.key = &kv.first;
+        auto it = m.nodes.find(kv.first);
+        e.now = it == m.nodes.end() ? nullptr : &it->second;
+        e.was = kv.second;
+        if (!e.now && e.was == PendingMap::kAbsent) continue;  // added and removed again
+        const uint32_t ifx = rd_le32(kv.first.md);
+        auto s = inc.slot_of.find(ifx);
+        if (s == inc.slot_of.end()) return full("new ifindex");
+        e.slot = s->second;
+        e.P = kv.first.plen - 32;
+        const uint8_t *ip = kv.first.md + 4;
+        e.hi = e.lo = 0;
+        for (int i = 0; i < 8; i++) e.hi = e.hi << 8 | ip[i];
+        for (int i = 8; i < 16; i++) e.lo = e.lo << 8 | ip[i];
+        e.a32 = (uint32_t)(e.hi >> 32);
+        if (e.P <= 32) {
+            any_short = true;
+            short_words += e.P <= 24 ? (1ull << (24 - e.P)) : 256;
+        }
+        edits.push_back(e);
+    }
+    if (any_short && h.short_mode != INFW_SHORT_DIR24) return full("short table is not DIR-24-8");
+    if (short_words > (1ull << 22)) return full("edits cover too much of the short table");
+
+    // IPv6 long prefixes: the final record set of every touched (slot, /32) group
+    struct Group {
+        uint64_t bucket;  // btab index (found or insert position)
+        bool found;
+        std::vector<infw_v6_rec> recs;
+    };
+    std::unordered_map<uint64_t, Group> groups;
+    const uint64_t bmask = h.btab.size() - 1;
+    uint64_t new_buckets = 0;
+    for (const Edit &e : edits) {
+        if (e.P <= 32) continue;
+        if (h.levels.empty()) return full("first long prefix");
+        const uint64_t gk = (uint64_t)e.slot << 32 | e.a32;
+        auto git = groups.find(gk);
+        if (git == groups.end()) {
+            Group g;
+            uint64_t i = infw_bucket_hash(e.slot, e.a32) & bmask;
+            for (;;) {
+                const infw_v6_bucket &b = h.btab[i];
+                if (b.tag == 0) {
+                    g.found = false;
+                    break;
+                }
+                if (b.tag == e.slot + 1 && b.top == e.a32) {
+                    g.found = true;
+                    break;
+                }
+                i = (i + 1) & bmask;
+            }
+            g.bucket = i;
+            if (g.found) {
+                const infw_v6_bucket &b = h.btab[i];
+                if (b.n == INFW_BUCKET_OVERFLOW) return full("edit in an overflowed IPv6 group");
+                g.recs.assign(b.rec, b.rec + b.n);
+            } else {
+                new_buckets++;
+            }
+            git = groups.emplace(gk, std::move(g)).first;
+        }
+        // replace this prefix's record (if any) by its current state
+        auto &rv = git->second.recs;
+        const uint32_t mid = (uint32_t)e.hi;
+        rv.erase(std::remove_if(rv.begin(), rv.end(),
+                                [&](const infw_v6_rec &r) { return (r.meta >> 25) == e.P - 32 && r.mid == mid && r.lo == e.lo; }),
+                 rv.end());
+        if (e.now) rv.push_back(infw_v6_rec{e.lo, mid, (e.P - 32) << 25});  // list filled in pass 2
+        if (rv.size() > INFW_BUCKET_INLINE) return full("IPv6 group exceeds 3 prefixes");
+    }
+    if ((h.n_buckets + new_buckets) * 2 > h.btab.size()) return full("IPv6 bucket table past half load");
+    // two new groups may share an insert position: they must not
+    {
+        std::vector<uint64_t> pos;
+        for (auto &kv : groups)
+            if (!kv.second.found && !kv.second.recs.empty()) pos.push_back(kv.second.bucket);
+        std::sort(pos.begin(), pos.end());
+        if (std::adjacent_find(pos.begin(), pos.end()) != pos.end()) return full("IPv6 bucket probe collision");
+    }
+
+    // lists: values not compiled yet, and the reference counts after the edits
+    std::vector<uint32_t> new_vids;
+    {
+        std::unordered_map<uint32_t, int> seen;
+        for (const Edit &e : edits)
+            if (e.now && !inc.list_of_vid.count(e.now->vid) && seen.emplace(e.now->vid, 0).second)
+                new_vids.push_back(e.now->vid);
+    }
+    const uint64_t n_lists_after = h.n_lists + new_vids.size();
+    if (n_lists_after >= (1u << 25)) return full("more than 2^25-1 rule lists");
+    std::unordered_map<uint32_t, int64_t> ref_delta;  // existing lists only
+    for (const Edit &e : edits) {
+        if (e.was != PendingMap::kAbsent) ref_delta[inc.list_of_vid.at((uint32_t)e.was)]--;
+        if (e.now) {
+            auto l = inc.list_of_vid.find(e.now->vid);
+            if (l != inc.list_of_vid.end()) ref_delta[l->second]++;
+        }
+    }
+    int64_t dead_after = (int64_t)inc.dead_lists;
+    for (const auto &d : ref_delta) {
+        const int64_t before = (int64_t)inc.list_refs[d.first], after = before + d.second;
+        dead_after += (after == 0) - (before == 0);
+    }
+    if (dead_after > 1024 && (uint64_t)dead_after * 2 > n_lists_after) return full("half of the rule lists are unreferenced");
+
+    // ---- pass 2: modify the image (nothing below can refuse)
+    const uint32_t n_lists_before = h.n_lists;
+    for (uint32_t vid : new_vids) {
+        const uint32_t lid = h.n_lists++;
+        inc.list_of_vid[vid] = lid;
+        inc.list_refs.push_back(0);
+        const size_t r0 = h.rules.size(), l0 = h.dtl.size();
+        // the image always holds >= 1 list slot: list 0 may be the placeholder of an empty epoch
+        if (h.desc.size() < (size_t)(lid + 1) * INFW_DESC_STRIDE) h.desc.resize((size_t)(lid + 1) * INFW_DESC_STRIDE, 0);
+        if (h.dte.size() < (size_t)(lid + 1) * INFW_NCLS) h.dte.resize((size_t)(lid + 1) * INFW_NCLS, infw_dt_line{});
+        int rc = compile_rule_list(m.pool.vals[vid].data(), h.rules, &h.desc[(size_t)lid * INFW_DESC_STRIDE],
+                                   &h.dte[(size_t)lid * INFW_NCLS], h.dtl);
+        if (rc) {
+            inc.valid = false;  // the image is no longer trustworthy: the next commit recompiles
+            set_error("incremental commit: decision-table leaf pool exhausted");
+            return rc;
+        }
+        mark(ranges, TB_DESC, (uint64_t)lid * INFW_DESC_STRIDE * sizeof(uint64_t), INFW_DESC_STRIDE * sizeof(uint64_t));
+        mark(ranges, TB_DTE, (uint64_t)lid * INFW_NCLS * sizeof(infw_dt_line), INFW_NCLS * sizeof(infw_dt_line));
+        mark(ranges, TB_RULES, r0 * sizeof(uint64_t), (h.rules.size() - r0) * sizeof(uint64_t));
+        mark(ranges, TB_DTL, l0 * sizeof(infw_dt_line), (h.dtl.size() - l0) * sizeof(infw_dt_line));
+    }
+    for (const Edit &e : edits)  // references of the lists just created (ref_delta holds the older ones)
+        if (e.now && inc.list_of_vid.at(e.now->vid) >= n_lists_before) inc.list_refs[inc.list_of_vid.at(e.now->vid)]++;
+    for (const auto &d : ref_delta) inc.list_refs[d.first] = (uint64_t)((int64_t)inc.list_refs[d.first] + d.second);
+    inc.dead_lists = (uint64_t)dead_after;
+    auto list1 = [&](const NodeVal *v) -> uint32_t { return v ? inc.list_of_vid.at(v->vid) + 1 : 0u; };
+
+    // <= /32: shorter prefixes first, so a /25../32 group starts from its final tbl24 word
+    std::vector<const Edit *> shorts;
+    for (const Edit &e : edits)
+        if (e.P <= 32) shorts.push_back(&e);
+    std::sort(shorts.begin(), shorts.end(), [](const Edit *a, const Edit *b) { return a->P < b->P; });
+    uint8_t md[20];
+    auto refill_group = [&](const uint8_t *ifx, uint32_t i24, uint32_t g, uint32_t j0, uint32_t cnt) {
+        uint32_t *t8 = &h.tbl8[(size_t)g << 8];
+        for (uint32_t j = j0; j < j0 + cnt; j++) {
+            short_md(md, ifx, i24 << 8 | j);
+            t8[j] = list1(m.longest(md, 32, 64));
+        }
+        mark(ranges, TB_TBL8, (((uint64_t)g << 8) + j0) * 4, (uint64_t)cnt * 4);
+    };
+    for (const Edit *e : shorts) {
+        const uint8_t *ifx = e->key->md;
+        uint32_t *t24 = &h.tbl24[(size_t)e->slot << 24];
+        if (e->P <= 24) {
+            const uint32_t i0 = e->a32 >> 8, cnt = 1u << (24 - e->P);
+            for (uint32_t i = i0; i < i0 + cnt; i++) {
+                const uint32_t w = t24[i];
+                if (w & INFW_TBL8_FLAG) {
+                    refill_group(ifx, i, w & ~INFW_TBL8_FLAG, 0, 256);
+                } else {
+                    short_md(md, ifx, i << 8);
+                    t24[i] = list1(m.longest(md, 32, 56));
+                }
+            }
+            mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i0) * 4, (uint64_t)cnt * 4);
+        } else {
+            const uint32_t i = e->a32 >> 8, w = t24[i];
+            uint32_t g;
+            if (w & INFW_TBL8_FLAG) {
+                g = w & ~INFW_TBL8_FLAG;
+            } else {
+                if (!e->now) continue;  // nothing below /24 here, nothing to remove
+                g = (uint32_t)(h.tbl8.size() >> 8);  // groups are never freed: a uniform one is harmless
+                h.tbl8.resize(h.tbl8.size() + 256, 0);
+                std::fill(h.tbl8.begin() + ((size_t)g << 8), h.tbl8.begin() + ((size_t)g << 8) + 256, w);
+                mark(ranges, TB_TBL8, ((uint64_t)g << 8) * 4, 256 * 4);
+                t24[i] = INFW_TBL8_FLAG | g;
+                mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 4, 4);
+                h.n_tbl8_groups++;
+            }
+            refill_group(ifx, i, g, e->a32 & 0xFFu, 1u << (32 - e->P));
+        }
+    }
+
+    // IPv6 buckets
+    std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
+    for (const auto &kv : inc.slot_of) ifx_of_slot[kv.second] = kv.first;
+    for (auto &kv : groups) {
+        Group &g = kv.second;
+        if (!g.found && g.recs.empty()) continue;
+        const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
+        for (infw_v6_rec &r : g.recs) {
+            uint8_t kmd[20];
+            // the record's entry: {ifindex, address bits 0..127} at its length
+            const uint32_t L = (r.meta >> 25) + 32;
+            memset(kmd, 0, 20);
+            memcpy(kmd, &ifx_of_slot[slot], 4);
+            const uint64_t hi = (uint64_t)top << 32 | r.mid;
+            for (int i = 0; i < 8; i++) kmd[4 + i] = (uint8_t)(hi >> (56 - 8 * i));
+            for (int i = 0; i < 8; i++) kmd[12 + i] = (uint8_t)(r.lo >> (56 - 8 * i));
+            const NodeVal *v = m.longest(kmd, L + 32, L + 32);
+            r.meta = (L - 32) << 25 | list1(v);
+        }
+        std::sort(g.recs.begin(), g.recs.end(), [](const infw_v6_rec &a, const infw_v6_rec &c) { return a.meta > c.meta; });
+        infw_v6_bucket &b = h.btab[g.bucket];
+        if (!g.found) {
+            b.tag = slot + 1;
+            b.top = top;
+            h.n_buckets++;
+        }
+        b.n = (uint32_t)g.recs.size();
+        memset(b.rec, 0, sizeof(b.rec));
+        for (size_t k = 0; k < g.recs.size(); k++) b.rec[k] = g.recs[k];
+        mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
+    }
+    h.n_entries = m.nodes.size();
+    return 0;
+}
+
+}  // namespace infw

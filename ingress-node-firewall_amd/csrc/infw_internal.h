@@ -52,11 +52,18 @@ struct PendingMap {
     uint64_t len_count[INFW_MAX_PREFIXLEN + 1] = {};
     ValuePool pool;
     uint64_t generation = 0;  // bumped on every successful edit
+    // Keys edited since the last commit -> their committed value id (kAbsent: the
+    // key was not in the committed set).  Drives the incremental commit.
+    static constexpr int64_t kAbsent = -1;
+    std::unordered_map<NodeKey, int64_t, NodeKeyHash> dirty;
 
     int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
     int remove(const lpm_ip_key_st *key);
     int lookup(const lpm_ip_key_st *key, uint8_t *val) const;
     int next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const;
+    // Longest entry with minlen <= prefixLen <= maxlen covering md (20 bytes:
+    // ifindex LE + address): its node, or nullptr.
+    const NodeVal *longest(const uint8_t md[20], uint32_t minlen, uint32_t maxlen) const;
 };
 
 void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes);
@@ -87,9 +94,37 @@ struct HostTables {
     infw_dev_tables view() const;
 };
 
+// Bookkeeping of the compiled image that an incremental commit patches
+// (incremental.cpp); filled by compile_tables.
+struct IncState {
+    bool valid = false;
+    std::unordered_map<uint32_t, uint32_t> slot_of;      // ifindex -> slot
+    std::unordered_map<uint32_t, uint32_t> list_of_vid;  // interned value -> rule list
+    std::vector<uint64_t> list_refs;                     // entries referencing each list
+    uint64_t dead_lists = 0;                             // lists no entry references any more
+};
+
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
 int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,
-                   uint64_t dir24_budget = 4ull << 30);
+                   uint64_t dir24_budget = 4ull << 30, IncState *inc = nullptr);
+
+// The device-resident buffers of one image, in upload order.
+enum TableBuf {
+    TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_COUNT
+};
+// Host bytes of buffer b (at least one element, like the upload).
+void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);
+struct DirtyRange {
+    uint32_t buf;
+    uint64_t off, len;  // bytes
+};
+// Apply m.dirty to the compiled image in place (DIR-24-8 words and tbl8 groups,
+// IPv6 buckets, appended rule lists), recording every byte range it changes.
+// Returns 0 when patched, 1 when the edit needs a full compile (*why says why;
+// nothing was modified), < 0 on error.
+int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
+                 std::string *why);
 
 // Class-filtered GPU rule records of one 1200-B value (appended to rules) and
 // the per-class first-match decision-table entry lines (leaf lines appended to leaves).

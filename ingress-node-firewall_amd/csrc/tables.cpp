@@ -103,6 +103,7 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
     auto it = nodes.find(k);
     if (it != nodes.end()) {
         if (flags == INFW_BPF_NOEXIST) return -EEXIST;
+        dirty.emplace(k, (int64_t)it->second.vid);  // keeps the committed state of the first edit
         memcpy(it->second.data, &key->ingress_ifindex, 4);
         memcpy(it->second.data + 4, key->ip_data, 16);
         it->second.vid = pool.intern(val);
@@ -118,6 +119,7 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
     memcpy(v.data, &key->ingress_ifindex, 4);
     memcpy(v.data + 4, key->ip_data, 16);
     v.vid = pool.intern(val);
+    dirty.emplace(k, kAbsent);
     nodes.emplace(k, v);
     order.insert(k);
     len_count[k.plen]++;
@@ -130,6 +132,7 @@ int PendingMap::remove(const lpm_ip_key_st *key) {
     NodeKey k = make_node(key);
     auto it = nodes.find(k);
     if (it == nodes.end()) return -ENOENT;
+    dirty.emplace(k, (int64_t)it->second.vid);
     nodes.erase(it);
     order.erase(k);
     len_count[k.plen]--;
@@ -154,6 +157,18 @@ int PendingMap::lookup(const lpm_ip_key_st *key, uint8_t *val) const {
         }
     }
     return -ENOENT;
+}
+
+const NodeVal *PendingMap::longest(const uint8_t md[20], uint32_t minlen, uint32_t maxlen) const {
+    for (int L = (int)maxlen; L >= (int)minlen; L--) {
+        if (!len_count[L]) continue;
+        NodeKey k;
+        k.plen = (uint32_t)L;
+        mask_bits(md, (uint32_t)L, k.md, 20);
+        auto it = nodes.find(k);
+        if (it != nodes.end()) return &it->second;
+    }
+    return nullptr;
 }
 
 int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
@@ -390,7 +405,7 @@ struct ShortEnt {
 };
 }  // namespace
 
-int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uint64_t dir24_budget) {
+int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uint64_t dir24_budget, IncState *inc) {
     out = HostTables();
     // --- slots: distinct ifindexes, ascending
     std::vector<uint32_t> ifs;
@@ -683,7 +698,42 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         }
         out.n_buckets = groups.size();
     }
+    if (inc) {
+        *inc = IncState();
+        inc->slot_of = std::move(slot_of);
+        inc->list_refs.assign(out.n_lists, 0);
+        for (const auto &kv : m.nodes) inc->list_refs[list_of_vid[kv.second.vid]]++;
+        inc->list_of_vid = std::move(list_of_vid);
+        inc->valid = true;
+    }
     return 0;
+}
+
+void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
+#define INFW_HB(v) \
+    *p = h.v.data(); \
+    *bytes = h.v.size() * sizeof(h.v[0]); \
+    break
+    switch (b) {
+    case TB_IFK: INFW_HB(if_keys);
+    case TB_IFS: INFW_HB(if_slot);
+    case TB_L16: INFW_HB(l16);
+    case TB_NODES: INFW_HB(nodes);
+    case TB_VPOOL: INFW_HB(vpool);
+    case TB_TBL24: INFW_HB(tbl24);
+    case TB_TBL8: INFW_HB(tbl8);
+    case TB_LTAB: INFW_HB(ltab);
+    case TB_BTAB: INFW_HB(btab);
+    case TB_DESC: INFW_HB(desc);
+    case TB_RULES: INFW_HB(rules);
+    case TB_DTE: INFW_HB(dte);
+    case TB_DTL: INFW_HB(dtl);
+    case TB_LEVELS: INFW_HB(levels);
+    default:
+        *p = nullptr;
+        *bytes = 0;
+    }
+#undef INFW_HB
 }
 
 infw_dev_tables HostTables::view() const {

@@ -5,7 +5,8 @@ Package layout (ingress-node-firewall_amd/):
   lib/      libinfw.so (product) and libinfw_workload.so (bench/test workloads), built in-tree
   infw/     this Python mirror of the reference's pkg/ebpf + pkg/metrics API over the C ABI
 """
-from ._native import (BPF_ANY, BPF_EXIST, BPF_NOEXIST, F_HOST_ONLY, F_KEEP_HOST_IMAGE, LIB_PATH, MAX_TARGETS,
+from ._native import (BPF_ANY, BPF_EXIST, BPF_NOEXIST, COMMIT_FULL, COMMIT_INCREMENTAL, COMMIT_REUPLOAD,
+                      F_FULL_COMMIT, F_HOST_ONLY, F_KEEP_HOST_IMAGE, LIB_PATH, MAX_TARGETS,
                       XDP_DROP, XDP_PASS, InfwError, LpmIpKeySt, RuleStatisticsSt, RulesValSt, RuleTypeSt)
 from .core import Classifier, build_ebpf_key, key_from_fields, verdicts_from_results
 from .controller import (IngNodeFwController, IngressNodeFirewallRules, ProtocolRule, Statistics,
@@ -15,5 +16,5 @@ __all__ = [
     "Classifier", "build_ebpf_key", "key_from_fields", "verdicts_from_results", "IngNodeFwController",
     "IngressNodeFirewallRules", "ProtocolRule", "Statistics", "make_rules_val", "LpmIpKeySt", "RulesValSt",
     "RuleTypeSt", "RuleStatisticsSt", "InfwError", "BPF_ANY", "BPF_NOEXIST", "BPF_EXIST", "F_HOST_ONLY",
-    "F_KEEP_HOST_IMAGE", "XDP_DROP", "XDP_PASS", "MAX_TARGETS", "LIB_PATH",
+    "F_KEEP_HOST_IMAGE", "F_FULL_COMMIT", "COMMIT_FULL", "COMMIT_INCREMENTAL", "COMMIT_REUPLOAD", "XDP_DROP", "XDP_PASS", "MAX_TARGETS", "LIB_PATH",
 ]

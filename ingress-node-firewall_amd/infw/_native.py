@@ -20,6 +20,8 @@ XDP_ABORTED, XDP_DROP, XDP_PASS = 0, 1, 2
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
 F_HOST_ONLY = 0x1
 F_KEEP_HOST_IMAGE = 0x2
+F_FULL_COMMIT = 0x4
+COMMIT_FULL, COMMIT_INCREMENTAL, COMMIT_REUPLOAD = 0, 1, 2
 HDR_SNAP = 80
 
 
@@ -103,7 +105,9 @@ class TableInfo(C.Structure):
                 ("n_lists", C.c_uint32), ("n_rules", C.c_uint64), ("n_tbl8_groups", C.c_uint64),
                 ("n_long_levels", C.c_uint32), ("n_long_entries", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double),
-                ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64)]
+                ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64),
+                ("commit_mode", C.c_uint32), ("pad0", C.c_uint32), ("patch_bytes", C.c_uint64),
+                ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12

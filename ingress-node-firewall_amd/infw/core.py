@@ -134,7 +134,9 @@ class Classifier:
     def info(self) -> Dict[str, float]:
         ti = N.TableInfo()
         check(N.lib.infw_table_info(self._ctx, C.byref(ti)), "info")
-        return {f: getattr(ti, f) for f, _ in N.TableInfo._fields_}
+        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f != "pad0"}
+        d["full_reason"] = ti.full_reason.decode()
+        return d
 
     # -- data path
     def classify_ptrs(self, dev: int, saddr: int, ifindex: int, pkt_len: int, meta: int, l4word: int, n: int,

@@ -337,3 +337,51 @@ def test_debug_lookup_capture():
     gpu_run(clf, batch, n)                       # full: new keys are dropped, the set is unchanged
     assert set(clf.debug_keys()) == set(got)
     assert np.array_equal(gres_b, m.classify_frames(hb, cb, pb, ib, nthreads=8)[0])
+
+
+def test_incremental_commits_on_device():
+    """§8f-2: a run of incremental commits (both device images ping-pong, one commit re-uploads
+    after its new rule lists outgrow the spare's buffers); after every commit the device results
+    equal the oracle's on the workload and on packets aimed at the edited prefixes."""
+    import random
+    from test_incremental_cpu import _apply, _packets_for, _val
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=100000, n_templates=512)
+    ents = list(wl.entries())
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)
+    m = orc.OracleMap(max_entries=wl.n_entries + 4096)
+    for k, v in ents:
+        _apply((clf,), m, k, v)
+    clf.commit()
+    dev = torch.device("cuda", 0)
+    n = 1 << 17
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 0, 0)
+    hdr, cap, pl, ifx = wl.frames(0, n)
+    rng = random.Random(17)
+    vals = [v for _, v in ents[:4000]]
+    modes = []
+    for step in range(7):
+        touched = []
+        n_new_vals = 1500 if step == 4 else 20
+        for k, _ in rng.sample(ents, 400 + n_new_vals):
+            if n_new_vals:
+                v = _val(rng, step)
+                n_new_vals -= 1
+            else:
+                v = None if rng.random() < 0.3 else rng.choice(vals)
+            _apply((clf,), m, k, v)
+            touched.append(k)
+        clf.commit()
+        info = clf.info()
+        modes.append(info["commit_mode"])
+        ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+        gres, _ = gpu_run(clf, batch, n)
+        assert np.array_equal(gres, ores), (step, info["commit_mode"])
+        th, tc, tp, ti = _packets_for(touched, rng, 2)
+        want, _, _, _ = m.classify_frames(th, tc, tp, ti, nthreads=8)
+        tb = SoaBatch.from_tuples(W.pack_frames(th, tc, tp, ti), dev)
+        got, _ = gpu_run(clf, tb, len(ti))
+        assert np.array_equal(got, want), (step, info["commit_mode"])
+        if info["commit_mode"] == infw.COMMIT_INCREMENTAL:
+            assert info["patch_bytes"] < (8 << 20), info["patch_bytes"]
+    assert modes.count(infw.COMMIT_INCREMENTAL) >= 4 and infw.COMMIT_REUPLOAD in modes, modes
