@@ -116,6 +116,32 @@ struct infw_ctx {
 
 static bool growable(int b) { return b == TB_TBL8 || b == TB_DESC || b == TB_RULES || b == TB_DTE || b == TB_DTL; }
 
+// Point the kernel's table view at an image's buffers.
+static void bind_view(DeviceEpoch &e, const HostTables &h) {
+    infw_dev_tables &t = e.view;
+    memset(&t, 0, sizeof(t));
+    t.if_keys = static_cast<const uint32_t *>(e.buf[TB_IFK]);
+    t.if_slot = static_cast<const uint32_t *>(e.buf[TB_IFS]);
+    t.l16 = static_cast<const uint32_t *>(e.buf[TB_L16]);
+    t.nodes = static_cast<const infw_bnode *>(e.buf[TB_NODES]);
+    t.vpool = static_cast<const uint32_t *>(e.buf[TB_VPOOL]);
+    t.tbl24 = static_cast<const uint32_t *>(e.buf[TB_TBL24]);
+    t.tbl8 = static_cast<const uint32_t *>(e.buf[TB_TBL8]);
+    t.ltab = static_cast<const infw_long_entry *>(e.buf[TB_LTAB]);
+    t.btab = static_cast<const infw_v6_bucket *>(e.buf[TB_BTAB]);
+    t.desc = static_cast<const uint64_t *>(e.buf[TB_DESC]);
+    t.rules = static_cast<const uint64_t *>(e.buf[TB_RULES]);
+    t.dte = static_cast<const infw_dt_line *>(e.buf[TB_DTE]);
+    t.dtl = static_cast<const infw_dt_line *>(e.buf[TB_DTL]);
+    t.levels = static_cast<const uint8_t *>(e.buf[TB_LEVELS]);
+    t.if_mask = (uint32_t)h.if_keys.size() - 1;
+    t.n_slots = h.n_slots;
+    t.lmask = h.ltab.size() - 1;
+    t.bmask = h.btab.size() - 1;
+    t.short_mode = h.short_mode;
+    t.n_levels = (uint32_t)h.levels.size();
+}
+
 static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {
     DeviceGuard g(ordinal);
     if (!g.ok) {
@@ -135,28 +161,29 @@ static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<Device
         ep->bytes += cap;
         if (bytes) HIP_OK(hipMemcpy(ep->buf[b], p, bytes, hipMemcpyHostToDevice));
     }
-    infw_dev_tables &t = ep->view;
-    memset(&t, 0, sizeof(t));
-    t.if_keys = static_cast<const uint32_t *>(ep->buf[TB_IFK]);
-    t.if_slot = static_cast<const uint32_t *>(ep->buf[TB_IFS]);
-    t.l16 = static_cast<const uint32_t *>(ep->buf[TB_L16]);
-    t.nodes = static_cast<const infw_bnode *>(ep->buf[TB_NODES]);
-    t.vpool = static_cast<const uint32_t *>(ep->buf[TB_VPOOL]);
-    t.tbl24 = static_cast<const uint32_t *>(ep->buf[TB_TBL24]);
-    t.tbl8 = static_cast<const uint32_t *>(ep->buf[TB_TBL8]);
-    t.ltab = static_cast<const infw_long_entry *>(ep->buf[TB_LTAB]);
-    t.btab = static_cast<const infw_v6_bucket *>(ep->buf[TB_BTAB]);
-    t.desc = static_cast<const uint64_t *>(ep->buf[TB_DESC]);
-    t.rules = static_cast<const uint64_t *>(ep->buf[TB_RULES]);
-    t.dte = static_cast<const infw_dt_line *>(ep->buf[TB_DTE]);
-    t.dtl = static_cast<const infw_dt_line *>(ep->buf[TB_DTL]);
-    t.levels = static_cast<const uint8_t *>(ep->buf[TB_LEVELS]);
-    t.if_mask = (uint32_t)h.if_keys.size() - 1;
-    t.n_slots = h.n_slots;
-    t.lmask = h.ltab.size() - 1;
-    t.bmask = h.btab.size() - 1;
-    t.short_mode = h.short_mode;
-    t.n_levels = (uint32_t)h.levels.size();
+    bind_view(*ep, h);
+    out = ep;
+    return 0;
+}
+
+// A second image with the same capacities and contents (device-to-device copy):
+// the spare an incremental commit patches.
+static int clone_epoch(const DeviceEpoch &src, const HostTables &h, std::shared_ptr<DeviceEpoch> &out) {
+    DeviceGuard g(src.ordinal);
+    if (!g.ok) return -ENODEV;
+    auto ep = std::make_shared<DeviceEpoch>();
+    ep->ordinal = src.ordinal;
+    for (int b = 0; b < TB_COUNT; b++) {
+        const void *p;
+        size_t bytes;
+        host_buffer(h, b, &p, &bytes);
+        HIP_OK(hipMalloc(&ep->buf[b], src.cap[b]));
+        ep->cap[b] = src.cap[b];
+        ep->bytes += src.cap[b];
+        if (bytes) HIP_OK(hipMemcpy(ep->buf[b], src.buf[b], bytes, hipMemcpyDeviceToDevice));
+    }
+    bind_view(*ep, h);
+    HIP_OK(hipDeviceSynchronize());
     out = ep;
     return 0;
 }
@@ -377,9 +404,10 @@ int infw_table_commit(infw_ctx *ctx) {
         rc = compile_tables(ctx->map, *h, smode, 4ull << 30, &inc);
         if (rc) return rc;  // the previous epoch stays live
         t1 = std::chrono::steady_clock::now();
-        std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size());
+        std::vector<std::shared_ptr<DeviceEpoch>> eps(ctx->devs.size()), spares(ctx->devs.size());
         for (size_t i = 0; i < ctx->devs.size(); i++) {
             rc = upload_epoch(*h, ctx->devs[i].ordinal, eps[i]);
+            if (!rc) rc = clone_epoch(*eps[i], *h, spares[i]);
             if (rc) return rc;  // nothing swapped: the previous epoch stays live
         }
         std::vector<std::shared_ptr<DeviceEpoch>> old;
@@ -389,7 +417,7 @@ int infw_table_commit(infw_ctx *ctx) {
                 old.push_back(ctx->devs[i].epoch);
                 old.push_back(ctx->devs[i].spare);
                 ctx->devs[i].epoch = eps[i];
-                ctx->devs[i].spare.reset();
+                ctx->devs[i].spare = spares[i];
             }
         }
         old.clear();  // waits for batches still running on the old images, then frees them
@@ -400,7 +428,7 @@ int infw_table_commit(infw_ctx *ctx) {
         t1 = std::chrono::steady_clock::now();
         const HostTables &h = *ctx->host_image;
         for (auto &d : ctx->devs) {
-            std::shared_ptr<DeviceEpoch> next;
+            std::shared_ptr<DeviceEpoch> next, fresh_spare;
             if (d.spare && image_fits(*d.spare, h)) {
                 // batches that took the spare while it was live have launched and finished
                 while (d.spare.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
@@ -417,9 +445,11 @@ int infw_table_commit(infw_ctx *ctx) {
                     return rc;
                 }
             } else {
-                rc = upload_epoch(h, d.ordinal, next);  // no spare yet, or it outgrew its buffers
+                // the patched host image outgrew the spare's buffers: a fresh pair from it
+                rc = upload_epoch(h, d.ordinal, next);
+                if (!rc) rc = clone_epoch(*next, h, fresh_spare);
                 if (rc) return rc;
-                if (d.spare) mode = INFW_COMMIT_REUPLOAD;
+                mode = INFW_COMMIT_REUPLOAD;
                 patched += next->bytes;
             }
             std::shared_ptr<DeviceEpoch> prev;
@@ -427,8 +457,8 @@ int infw_table_commit(infw_ctx *ctx) {
                 std::lock_guard<std::mutex> lk(ctx->epoch_mu);
                 prev = d.epoch;
                 d.epoch = next;
-                d.spare.reset();
-                if (prev && image_fits(*prev, h)) {
+                d.spare = fresh_spare;
+                if (!fresh_spare && prev && image_fits(*prev, h)) {
                     prev->pending.insert(prev->pending.end(), ranges.begin(), ranges.end());
                     d.spare = prev;
                 }

@@ -344,6 +344,7 @@ def test_incremental_commits_on_device():
     after its new rule lists outgrow the spare's buffers); after every commit the device results
     equal the oracle's on the workload and on packets aimed at the edited prefixes."""
     import random
+    import orc
     from test_incremental_cpu import _apply, _packets_for, _val
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=100000, n_templates=512)
     ents = list(wl.entries())
