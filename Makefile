@@ -53,4 +53,11 @@ asan:
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build
 
-.PHONY: all clean resource-usage asm asan
+.PHONY: all clean resource-usage asm asan cachesim
+
+# host model of the L2 behaviour of the table walk (layout experiments; tools/cachesim.cpp)
+cachesim: $(OUT)/libinfw_workload.so
+	@mkdir -p $(OBJ)
+	g++ -std=c++17 -O2 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/cachesim.cpp $(SRC)/tables.cpp \
+	    $(SRC)/incremental.cpp $(SRC)/controlplane.cpp -L$(OUT) -linfw_workload -Wl,-rpath,$(abspath $(OUT)) \
+	    -o $(OBJ)/cachesim

@@ -140,6 +140,7 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.bmask = h.btab.size() - 1;
     t.short_mode = h.short_mode;
     t.n_levels = (uint32_t)h.levels.size();
+    t.dt_plog2 = h.dt_plog2;
 }
 
 static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {

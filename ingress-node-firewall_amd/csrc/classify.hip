@@ -61,8 +61,8 @@ __device__ __forceinline__ uint32_t scan_tail(const uint64_t *__restrict__ rules
 // whole (four 16-B loads of one 64-B line, issued back to back).
 __device__ __forceinline__ uint32_t lt2(uint32_t w, uint32_t v) { return infw_count_lt(w, v); }
 __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
-                                              uint32_t list, int cls, uint32_t v) {
-    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + ((uint64_t)list * INFW_NCLS + (uint32_t)cls));
+                                              uint32_t list, int cls, uint32_t v, uint32_t plog2) {
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + infw_dt_slot(list, cls, v, plog2));
     u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
     if (a[0] & INFW_DT_ROOT) {
         const uint32_t g = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
         uint32_t result = 0;
         if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32) ^ lst;  // diagnostic 2: no first-match stage
-        else if (G == 0 && lst) result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val);
+        else if (G == 0 && lst) result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2);
         // ---- first match, one lane per rule, G packets in flight
         uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
         while (G > 0 && pending) {

@@ -190,16 +190,17 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         const size_t r0 = h.rules.size(), l0 = h.dtl.size();
         // the image always holds >= 1 list slot: list 0 may be the placeholder of an empty epoch
         if (h.desc.size() < (size_t)(lid + 1) * INFW_DESC_STRIDE) h.desc.resize((size_t)(lid + 1) * INFW_DESC_STRIDE, 0);
-        if (h.dte.size() < (size_t)(lid + 1) * INFW_NCLS) h.dte.resize((size_t)(lid + 1) * INFW_NCLS, infw_dt_line{});
+        const size_t per_list = (size_t)INFW_NCLS << h.dt_plog2;
+        if (h.dte.size() < (lid + 1) * per_list) h.dte.resize((lid + 1) * per_list, infw_dt_line{});
         int rc = compile_rule_list(m.pool.vals[vid].data(), h.rules, &h.desc[(size_t)lid * INFW_DESC_STRIDE],
-                                   &h.dte[(size_t)lid * INFW_NCLS], h.dtl);
+                                   &h.dte[lid * per_list], h.dtl, h.dt_plog2);
         if (rc) {
             inc.valid = false;  // the image is no longer trustworthy: the next commit recompiles
             set_error("incremental commit: decision-table leaf pool exhausted");
             return rc;
         }
         mark(ranges, TB_DESC, (uint64_t)lid * INFW_DESC_STRIDE * sizeof(uint64_t), INFW_DESC_STRIDE * sizeof(uint64_t));
-        mark(ranges, TB_DTE, (uint64_t)lid * INFW_NCLS * sizeof(infw_dt_line), INFW_NCLS * sizeof(infw_dt_line));
+        mark(ranges, TB_DTE, (uint64_t)lid * per_list * sizeof(infw_dt_line), per_list * sizeof(infw_dt_line));
         mark(ranges, TB_RULES, r0 * sizeof(uint64_t), (h.rules.size() - r0) * sizeof(uint64_t));
         mark(ranges, TB_DTL, l0 * sizeof(infw_dt_line), (h.dtl.size() - l0) * sizeof(infw_dt_line));
     }

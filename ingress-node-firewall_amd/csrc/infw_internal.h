@@ -87,6 +87,7 @@ struct HostTables {
     std::vector<uint64_t> desc;
     std::vector<uint64_t> rules;
     std::vector<infw_dt_line> dte, dtl;  // decision-table entry and leaf lines
+    uint32_t dt_plog2 = 0;               // value-axis parts per (list, class): 1 << dt_plog2
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -127,11 +128,17 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                  std::string *why);
 
 // Class-filtered GPU rule records of one 1200-B value (appended to rules) and
-// the per-class first-match decision-table entry lines (leaf lines appended to leaves).
+// the per-class first-match decision-table entry lines, INFW_NCLS << plog2 of
+// them (leaf lines appended to leaves).
 int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE],
-                      infw_dt_line entry_out[INFW_NCLS], std::vector<infw_dt_line> &leaves);
-// Decision table of one class list (records {lo16, hi16, result32} in scan order).
-int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry, std::vector<infw_dt_line> &leaves);
+                      infw_dt_line *entry_out, std::vector<infw_dt_line> &leaves, uint32_t plog2);
+// First-match step function of one class list (records {lo16, hi16, result32} in
+// scan order): segment starts ascending from 0 and the result of each segment.
+void step_function(const std::vector<uint64_t> &recs, std::vector<uint32_t> &starts, std::vector<uint32_t> &res);
+// Decision table of one class list (records {lo16, hi16, result32} in scan
+// order): 1 << plog2 entry lines, one per part of the value axis.
+int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line *entry, std::vector<infw_dt_line> &leaves,
+                         uint32_t plog2);
 // Entry (and leaf) lines of a step function: segment starts ascending from 0 and their results.
 int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
                         std::vector<infw_dt_line> &leaves);

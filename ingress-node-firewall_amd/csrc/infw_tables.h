@@ -78,11 +78,15 @@ struct infw_v6_bucket {     // 64 B
 
 // First-match decision tables.  For one (rule list, packet class) the
 // first-match result as a function of the 16-bit packet value (dport, or
-// type << 8 | code) is a step function with S <= 2c + 1 <= 201 segments.  It is
-// stored in 64-B lines (one L2 request each), so that a packet touches at most
-// two lines after the LPM answer:
-//   entry line   dte[list * INFW_NCLS + cls] — addressed directly from the LPM
-//                answer, no descriptor load in between;
+// type << 8 | code) is a step function with S <= 2c + 1 <= 201 segments.  The
+// value axis is cut into 2^dt_plog2 equal parts (16 by default, 1 when the
+// table would exceed its memory budget), and each part's piece of the step
+// function is stored from one 64-B line (one L2 request), so that a packet
+// touches one line after the LPM answer, two when its part holds more
+// segments than a leaf:
+//   entry line   dte[((list * INFW_NCLS + cls) << dt_plog2) | v >> (16 - dt_plog2)]
+//                — addressed directly from the LPM answer and the value, no
+//                descriptor load in between;
 //   leaf form    (w[0] bit 31 clear; S <= 10): u16 keys in w[1..5] (key j =
 //                start of segment j+1 minus 1, so "key < v" <=> "start <= v";
 //                pad 0xFFFF never counts) and the results in w[6..15]; the
@@ -145,6 +149,7 @@ struct infw_dev_tables {
     const struct infw_dt_line *dtl;  // decision mode: leaf lines
     const uint8_t *levels;     // n_levels distinct long lengths, ascending
     uint32_t n_levels;
+    uint32_t dt_plog2;         // decision-table parts per (list, class): 1 << dt_plog2 (0 or 4)
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -233,6 +238,11 @@ INFW_TD uint32_t infw_keys_below(const uint32_t *w, int a, int b, uint32_t v) {
     return c;
 }
 
+// Entry line of (list, cls) for value v.
+INFW_TD uint64_t infw_dt_slot(uint32_t list, int cls, uint32_t v, uint32_t plog2) {
+    return (((uint64_t)list * INFW_NCLS + (uint32_t)cls) << plog2) | (v >> (16u - plog2));
+}
+
 // Result word of a compact-leaf code (0 = no match).
 INFW_TD uint32_t infw_dt_code_result(uint32_t code) {
     return code ? ((code >> 1) << 8 | (1u + (code & 1u))) : 0u;
@@ -259,7 +269,7 @@ INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
 // First-match result of (list, cls) for value v (host walk; the kernel has its own loads).
 template <class T>
 INFW_TD uint32_t infw_dt_eval(const T &t, uint32_t list, int cls, uint32_t v) {
-    const uint32_t *w = t.dte[(uint64_t)list * INFW_NCLS + cls].w;
+    const uint32_t *w = t.dte[infw_dt_slot(list, cls, v, t.dt_plog2)].w;
     if (w[0] & INFW_DT_ROOT) w = t.dtl[(w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, v)].w;
     return infw_dt_leaf(w, v);
 }

@@ -263,11 +263,36 @@ int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<u
     return 0;
 }
 
-int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry, std::vector<infw_dt_line> &leaves) {
+int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line *entry, std::vector<infw_dt_line> &leaves,
+                         uint32_t plog2) {
+    std::vector<uint32_t> starts, res;
+    step_function(recs, starts, res);
+    const uint32_t span = 65536u >> plog2;
+    std::vector<uint32_t> ps, pr;
+    size_t j = 0;  // segment holding the part's first value
+    for (uint32_t q = 0; q < (1u << plog2); q++) {
+        const uint32_t lo = q * span, hi = lo + span;
+        while (j + 1 < starts.size() && starts[j + 1] <= lo) j++;
+        ps.assign(1, lo);
+        pr.assign(1, res[j]);
+        for (size_t k = j + 1; k < starts.size() && starts[k] < hi; k++) {
+            ps.push_back(starts[k]);
+            pr.push_back(res[k]);
+        }
+        const int rc = emit_decision_lines(ps, pr, entry[q], leaves);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+void step_function(const std::vector<uint64_t> &recs, std::vector<uint32_t> &starts, std::vector<uint32_t> &res) {
+    starts.clear();
+    res.clear();
     const size_t c = recs.size();
     if (c == 0) {
-        const std::vector<uint32_t> z0{0}, r0{0};
-        return emit_decision_lines(z0, r0, entry, leaves);
+        starts.push_back(0);
+        res.push_back(0);
+        return;
     }
     std::vector<std::pair<uint32_t, uint32_t>> ev;  // (position, rule index) starts
     std::vector<std::pair<uint32_t, uint32_t>> en;  // (position, rule index) ends (hi + 1)
@@ -287,7 +312,6 @@ int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry,
     std::sort(en.begin(), en.end());
     std::vector<uint8_t> active(c, 0);
     std::priority_queue<uint32_t, std::vector<uint32_t>, std::greater<uint32_t>> heap;
-    std::vector<uint32_t> starts, res;
     size_t ie = 0, in = 0;
     for (uint32_t p : pts) {
         while (in < en.size() && en[in].first == p) active[en[in++].second] = 0;
@@ -302,12 +326,11 @@ int build_decision_table(const std::vector<uint64_t> &recs, infw_dt_line &entry,
             res.push_back(r);
         }
     }
-    return emit_decision_lines(starts, res, entry, leaves);
 }
 
 int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
-                      uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line entry_out[INFW_NCLS],
-                      std::vector<infw_dt_line> &leaves) {
+                      uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line *entry_out,
+                      std::vector<infw_dt_line> &leaves, uint32_t plog2) {
     int rc = 0;
     std::vector<uint64_t> per[INFW_NCLS];
     for (int i = 0; i < INFW_MAX_RULES_PER_TARGET; i++) {
@@ -346,7 +369,7 @@ int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
         }
     }
     for (int c = 0; c < INFW_DESC_STRIDE; c++) {
-        if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], entry_out[c], leaves);
+        if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], &entry_out[(size_t)c << plog2], leaves, plog2);
         if (c >= INFW_NCLS || per[c].empty()) {
             desc_out[c] = 0;
             continue;
@@ -448,7 +471,10 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     }
     out.n_lists = (uint32_t)list_of_vid.size();
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
-    out.dte.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS, infw_dt_line{});
+    // 16 parts per (list, class) while the entry lines fit 1 GiB (INFW_DT_PARTS=1|16 forces one form)
+    out.dt_plog2 = (uint64_t)out.n_lists * INFW_NCLS * 16 * sizeof(infw_dt_line) <= (1ull << 30) ? 4 : 0;
+    if (const char *e = getenv("INFW_DT_PARTS")) out.dt_plog2 = atoi(e) == 16 ? 4 : atoi(e) == 1 ? 0 : out.dt_plog2;
+    out.dte.assign(((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS) << out.dt_plog2, infw_dt_line{});
     out.dtl.clear();
     int dt_rc = 0;
     {
@@ -460,8 +486,8 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         for (auto &p : by_lid)
             if (!dt_rc)
                 dt_rc = compile_rule_list(m.pool.vals[p.first].data(), out.rules,
-                                          &out.desc[(size_t)p.second * INFW_DESC_STRIDE], &out.dte[(size_t)p.second * INFW_NCLS],
-                                          out.dtl);
+                                          &out.desc[(size_t)p.second * INFW_DESC_STRIDE],
+                                          &out.dte[((size_t)p.second * INFW_NCLS) << out.dt_plog2], out.dtl, out.dt_plog2);
     }
     if (dt_rc) {
         set_error("compile: decision-table leaf pool exceeds 2^31 lines");
@@ -759,6 +785,7 @@ infw_dev_tables HostTables::view() const {
     t.dtl = dtl.data();
     t.n_levels = (uint32_t)levels.size();
     t.levels = levels.data();
+    t.dt_plog2 = dt_plog2;
     return t;
 }
 

@@ -1,0 +1,199 @@
+// cachesim.cpp — L2 behaviour of the classify kernel's table walk, on the host.
+//
+// Builds the configs[2] tables with the product's compiler, generates packets
+// with the workload generator, walks each packet the way the kernel does and
+// feeds every table line it touches into a model of the MI355X L2: 8 XCDs x
+// 4 MiB, 16-way, 128-B lines, LRU; packet i runs on XCD (i / 512) % 8 (tiles of
+// 512 packets striped over workgroups, workgroups round-robin over XCDs).
+// Reports L2 requests / misses per packet per structure, for the compiled layout
+// ("current"; INFW_DT_PARTS / INFW_DT_FORM select it) and for candidate layouts
+// expressed as alternative address maps over the single-part layout
+// (INFW_DT_PARTS=1):
+//   tbl24_u16   DIR-24-8 words of 2 bytes
+//   entry32     decision entries of 32 B, a list's classes packed in 128-B lines
+//   quartersQ / partsQxB   entry lines addressed by (list, class, value part)
+// Build + run: make cachesim   (tools/cachesim [n_packets])
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
+
+#include "../ingress-node-firewall_amd/csrc/infw_internal.h"
+#include "../ingress-node-firewall_amd/csrc/workload.h"
+
+namespace infw {
+void set_error(const std::string &s) { fprintf(stderr, "set_error: %s\n", s.c_str()); }
+}  // namespace infw
+using namespace infw;
+
+namespace {
+
+struct L2 {
+    static constexpr int kWays = 16, kLine = 128;
+    uint32_t sets;
+    std::vector<uint64_t> tag;  // sets x ways, most recent first
+    explicit L2(uint64_t bytes) : sets((uint32_t)(bytes / kLine / kWays)), tag((size_t)sets * kWays, ~0ull) {}
+    bool access(uint64_t addr) {  // true = hit
+        const uint64_t line = addr / kLine;
+        const uint64_t h = line * 0x9E3779B97F4A7C15ull;
+        uint64_t *t = &tag[(size_t)((h >> 32) % sets) * kWays];
+        for (int w = 0; w < kWays; w++)
+            if (t[w] == line) {
+                for (int k = w; k > 0; k--) t[k] = t[k - 1];
+                t[0] = line;
+                return true;
+            }
+        for (int k = kWays - 1; k > 0; k--) t[k] = t[k - 1];
+        t[0] = line;
+        return false;
+    }
+};
+
+enum Struct { S_BUCKET, S_TBL24, S_TBL8, S_ENTRY, S_LEAF, S_N };
+const char *kName[S_N] = {"bucket", "tbl24", "tbl8", "entry", "leaf"};
+
+struct Touch {
+    int s;
+    uint64_t addr;
+};
+
+// Separate virtual address spaces per structure (1 TiB apart).
+constexpr uint64_t kSpace = 1ull << 40;
+
+struct Variant {
+    const char *name;
+    bool tbl24_u16, entry32;
+    int quarters;  // > 0: decision lines addressed by (list, class, value >> (16 - log2 quarters))
+    int slot_bytes = 64;  // bytes per (list, class, part) slot: a compact leaf of 20 / 10 / 5 segments
+    int entry_stride = 64;
+};
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (4u << 20);
+    infw_wl *wl = nullptr;
+    if (infw_wl_create(&wl, INFW_WL_CFG2_MIXED_1M, 0x1F000002ull, 0, 0)) return 1;
+    PendingMap m;
+    m.max_entries = 1u << 22;
+    const uint64_t ne = infw_wl_n_entries(wl);
+    const lpm_ip_key_st *keys = infw_wl_keys(wl);
+    const uint32_t *vi = infw_wl_val_index(wl);
+    const rulesVal_st *tv = infw_wl_templates(wl);
+    for (uint64_t i = 0; i < ne; i++) m.update(&keys[i], reinterpret_cast<const uint8_t *>(&tv[vi[i]]), 0);
+    HostTables h;
+    if (compile_tables(m, h, 0)) return 2;
+    const infw_dev_tables t = h.view();
+    std::vector<uint32_t> tup(n * 8);
+    infw_wl_tuples(wl, 0, n, tup.data(), 8);
+
+    // per (list, class): the step function, for the quartered variants
+    std::vector<std::vector<uint32_t>> seg_starts((size_t)h.n_lists * INFW_NCLS);
+    for (uint32_t l = 0; l < h.n_lists; l++)
+        for (int c = 0; c < INFW_NCLS; c++) {
+            const uint64_t d = h.desc[(size_t)l * INFW_DESC_STRIDE + c];
+            std::vector<uint64_t> recs(h.rules.begin() + (uint32_t)d, h.rules.begin() + (uint32_t)d + (d >> 32));
+            std::vector<uint32_t> st, rs;
+            step_function(recs, st, rs);
+            seg_starts[(size_t)l * INFW_NCLS + c] = st;
+        }
+    const Variant vars[] = {{"current", false, false, 0}, {"tbl24_u16", true, false, 0}, {"entry32", false, true, 0},
+                            {"quarters4", false, false, 4}, {"quarters8", false, false, 8},
+                            {"quarters16", false, false, 16}, {"parts16x32B", false, false, 16, 32},
+                            {"parts32x32B", false, false, 32, 32}, {"parts32x16B", false, false, 32, 16},
+                            {"parts64x16B", false, false, 64, 16}, {"parts8x32B", false, false, 8, 32},
+                            {"stride128", false, false, 0, 64, 128}};
+    for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
+        uint64_t parts = 0, over = 0;
+        for (const auto &st : seg_starts)
+            for (int q = 0; q < Q; q++) {
+                const uint32_t lo = (uint32_t)q * (65536 / Q), hi = lo + 65536 / Q;
+                uint32_t nseg = 1;
+                for (uint32_t x : st) nseg += x > lo && x < hi;
+                parts++;
+                over += nseg > INFW_DT_CLEAF_SEGS;
+            }
+        printf("{\"parts\": %d, \"lines\": %llu, \"over_20_segments\": %llu}\n", Q, (unsigned long long)parts,
+               (unsigned long long)over);
+    }
+    for (const Variant &V : vars) {
+        std::vector<L2> l2(8, L2(4ull << 20));
+        uint64_t req[S_N] = {}, miss[S_N] = {};
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            const int pk = infw_parse(q[6], q[7], &cls, &val);
+            if (pk < INFW_PK_V4) continue;
+            Touch tc[6];
+            int nt = 0;
+            const int slot = infw_if_slot(t, q[4]);
+            uint32_t l1 = 0;
+            if (slot >= 0) {
+                const uint32_t a32 = infw_bswap32(q[0]);
+                uint32_t lng = 0;
+                if (pk == INFW_PK_V6 && t.n_levels) {
+                    const uint64_t bi = infw_bucket_hash((uint32_t)slot, a32) & t.bmask;  // first probe only
+                    tc[nt++] = {S_BUCKET, 0 * kSpace + bi * 64};
+                    lng = infw_v6_long(t, (uint32_t)slot, a32, q);
+                }
+                if (!lng) {
+                    const uint64_t w = ((uint64_t)slot << 24) | (a32 >> 8);
+                    tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 4)};
+                    uint32_t e = t.tbl24[w];
+                    if (e & INFW_TBL8_FLAG) {
+                        const uint64_t w8 = ((uint64_t)(e & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu);
+                        tc[nt++] = {S_TBL8, 2 * kSpace + w8 * (V.tbl24_u16 ? 2 : 4)};
+                        e = t.tbl8[w8];
+                    }
+                    l1 = e;
+                } else {
+                    l1 = lng;
+                }
+            }
+            if (l1 && V.quarters) {
+                const uint64_t ei = (uint64_t)(l1 - 1) * INFW_NCLS + cls;
+                const uint32_t Q = (uint32_t)V.quarters, q = val / (65536 / Q);
+                const uint32_t cap = V.slot_bytes == 64 ? 20 : V.slot_bytes == 32 ? 10 : 5;
+                tc[nt++] = {S_ENTRY, 3 * kSpace + (ei * Q + q) * V.slot_bytes};
+                const auto &st = seg_starts[ei];
+                const uint32_t lo = q * (65536 / Q), hi = lo + 65536 / Q;
+                uint32_t nseg = 1, below = 0;
+                for (uint32_t x : st) {
+                    nseg += x > lo && x < hi;
+                    below += x > lo && x <= val;
+                }
+                if (nseg > cap)  // root in the slot, then one leaf of 20 segments
+                    tc[nt++] = {S_LEAF, 4 * kSpace + ((ei * Q + q) * 16 + below / INFW_DT_CLEAF_SEGS) * 64};
+            } else if (l1) {
+                const uint64_t ei = (uint64_t)(l1 - 1) * INFW_NCLS + cls;
+                // entry32: a list's 7 classes in 256 B (TCP, UDP, SCTP, ICMP4 | ICMP6, 58/v4, 1/v6)
+                tc[nt++] = {S_ENTRY, 3 * kSpace + (V.entry32 ? (uint64_t)(l1 - 1) * 256 + cls * 32 : ei * V.entry_stride)};
+                const uint64_t slot_i = infw_dt_slot(l1 - 1, cls, val, t.dt_plog2);
+                if (t.dt_plog2) tc[nt - 1].addr = 3 * kSpace + slot_i * 64;  // the compiled layout's entry line
+                const uint32_t *w = t.dte[slot_i].w;
+                if (w[0] & INFW_DT_ROOT) {
+                    const uint64_t li = (w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, val);
+                    tc[nt++] = {S_LEAF, 4 * kSpace + li * 64};
+                }
+            }
+            L2 &c = l2[(i / 512) % 8];
+            for (int k = 0; k < nt; k++) {
+                req[tc[k].s]++;
+                if (!c.access(tc[k].addr)) miss[tc[k].s]++;
+            }
+        }
+        double tr = 0, tm = 0;
+        printf("{\"variant\": \"%s\", \"packets\": %llu", V.name, (unsigned long long)n);
+        for (int s = 0; s < S_N; s++) {
+            printf(", \"%s\": [%.4f, %.4f]", kName[s], (double)req[s] / n, (double)miss[s] / n);
+            tr += (double)req[s] / n;
+            tm += (double)miss[s] / n;
+        }
+        printf(", \"requests\": %.4f, \"misses\": %.4f}\n", tr, tm);
+        fflush(stdout);
+    }
+    infw_wl_destroy(wl);
+    return 0;
+}
