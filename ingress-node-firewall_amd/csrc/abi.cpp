@@ -125,7 +125,7 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.l16 = static_cast<const uint32_t *>(e.buf[TB_L16]);
     t.nodes = static_cast<const infw_bnode *>(e.buf[TB_NODES]);
     t.vpool = static_cast<const uint32_t *>(e.buf[TB_VPOOL]);
-    t.tbl24 = static_cast<const uint32_t *>(e.buf[TB_TBL24]);
+    t.tbl24 = static_cast<const uint64_t *>(e.buf[TB_TBL24]);
     t.tbl8 = static_cast<const uint32_t *>(e.buf[TB_TBL8]);
     t.ltab = static_cast<const infw_long_entry *>(e.buf[TB_LTAB]);
     t.btab = static_cast<const infw_v6_bucket *>(e.buf[TB_BTAB]);

@@ -226,35 +226,39 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     };
     for (const Edit *e : shorts) {
         const uint8_t *ifx = e->key->md;
-        uint32_t *t24 = &h.tbl24[(size_t)e->slot << 24];
+        uint64_t *t24 = &h.tbl24[(size_t)e->slot << 24];
+        const uint64_t gkey = (uint64_t)e->slot << 24;
         if (e->P <= 24) {
             const uint32_t i0 = e->a32 >> 8, cnt = 1u << (24 - e->P);
             for (uint32_t i = i0; i < i0 + cnt; i++) {
-                const uint32_t w = t24[i];
-                if (w & INFW_TBL8_FLAG) {
-                    refill_group(ifx, i, w & ~INFW_TBL8_FLAG, 0, 256);
+                auto g = h.tbl8_of.find(gkey | i);
+                if (g != h.tbl8_of.end()) {
+                    refill_group(ifx, i, g->second, 0, 256);
+                    t24[i] = infw_d24_encode(&h.tbl8[(size_t)g->second << 8], g->second, h.d24_inline);
                 } else {
                     short_md(md, ifx, i << 8);
                     t24[i] = list1(m.longest(md, 32, 56));
                 }
             }
-            mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i0) * 4, (uint64_t)cnt * 4);
+            mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i0) * 8, (uint64_t)cnt * 8);
         } else {
-            const uint32_t i = e->a32 >> 8, w = t24[i];
+            const uint32_t i = e->a32 >> 8;
+            auto it = h.tbl8_of.find(gkey | i);
             uint32_t g;
-            if (w & INFW_TBL8_FLAG) {
-                g = w & ~INFW_TBL8_FLAG;
+            if (it != h.tbl8_of.end()) {
+                g = it->second;
             } else {
                 if (!e->now) continue;  // nothing below /24 here, nothing to remove
                 g = (uint32_t)(h.tbl8.size() >> 8);  // groups are never freed: a uniform one is harmless
                 h.tbl8.resize(h.tbl8.size() + 256, 0);
-                std::fill(h.tbl8.begin() + ((size_t)g << 8), h.tbl8.begin() + ((size_t)g << 8) + 256, w);
+                std::fill(h.tbl8.begin() + ((size_t)g << 8), h.tbl8.begin() + ((size_t)g << 8) + 256, (uint32_t)t24[i]);
                 mark(ranges, TB_TBL8, ((uint64_t)g << 8) * 4, 256 * 4);
-                t24[i] = INFW_TBL8_FLAG | g;
-                mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 4, 4);
+                h.tbl8_of[gkey | i] = g;
                 h.n_tbl8_groups++;
             }
             refill_group(ifx, i, g, e->a32 & 0xFFu, 1u << (32 - e->P));
+            t24[i] = infw_d24_encode(&h.tbl8[(size_t)g << 8], g, h.d24_inline);
+            mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 8, 8);
         }
     }
 

@@ -78,7 +78,10 @@ struct HostTables {
     std::vector<infw_bnode> nodes;
     std::vector<uint32_t> vpool;
     uint64_t n_tbl8_groups = 0;   // DIR-24-8 second-level groups of the build image
-    std::vector<uint32_t> tbl24, tbl8;  // DIR-24-8 form (short_mode == INFW_SHORT_DIR24)
+    std::vector<uint64_t> tbl24;        // DIR-24-8 form (short_mode == INFW_SHORT_DIR24), INFW_D24_* words
+    std::vector<uint32_t> tbl8;         // 256-value groups of every /24 with entries longer than /24
+    std::unordered_map<uint64_t, uint32_t> tbl8_of;  // slot << 24 | /24 -> its group (inline words too)
+    bool d24_inline = true;             // INFW_D24_INLINE=0: every group stays in tbl8 (A/B)
     uint32_t short_mode = INFW_SHORT_DIR24;
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;

@@ -11,9 +11,10 @@
 //
 // How the epoch lays that out in HBM (built on the host, tables.cpp):
 //   ifindex -> slot      open-addressed u32 table
-//   short (<= /32)       DIR-24-8 per slot: tbl24[slot][2^24] u32 + tbl8 groups
-//                        of 256 u32; value = list+1 (0 = no entry), bit 31 of a
-//                        tbl24 word = "tbl8 group index"
+//   short (<= /32)       DIR-24-8 per slot: tbl24[slot][2^24] u64 + tbl8 groups
+//                        of 256 u32; value = list+1 (0 = no entry); a /24 with
+//                        longer entries is held inline in its tbl24 word when
+//                        it has <= 3 runs (almost always), else in a tbl8 group
 //   long  (/33../128)    one open-addressed table of 32-B records keyed by
 //                        (slot, length, masked address), searched by binary
 //                        search over the distinct lengths with markers
@@ -136,7 +137,7 @@ struct infw_dev_tables {
     const uint32_t *l16;       // n_slots << 16
     const struct infw_bnode *nodes;
     const uint32_t *vpool;
-    const uint32_t *tbl24;     // DIR-24-8 form: n_slots << 24 words + tbl8 groups
+    const uint64_t *tbl24;     // DIR-24-8 form: n_slots << 24 words (INFW_D24_*) + tbl8 groups
     const uint32_t *tbl8;
     uint32_t short_mode;       // INFW_SHORT_DIR24 or INFW_SHORT_COMPRESSED
     const struct infw_long_entry *ltab;
@@ -315,11 +316,52 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 #define INFW_SHORT_COMPRESSED 1u
 #define INFW_SHORT_NONE 2u        // DIR-24-8 build without any <= /32 entry
 
+// DIR-24-8 word (8 B).  Bits 63..62:
+//   00  plain: list+1 of the whole /24 in bits 0..31;
+//   10  tbl8 group index in bits 0..31 (256 u32 values, one per last byte);
+//   11  inline /24 of <= 3 runs, values <= 0x7FFF: v0 bits 0..14, v1 15..29,
+//       v2 30..44, run starts b1 bits 45..52 and b2 53..60 (b1 <= b2): last
+//       byte x -> x < b1 ? v0 : x < b2 ? v1 : v2.  One 8-B word instead of a
+//       second, dependent L2 request into a tbl8 group.
+#define INFW_D24_GROUP (1ull << 63)
+#define INFW_D24_INLINE (1ull << 62)
+#define INFW_D24_MAXV 0x7FFFu
+
+// Word for a /24 whose 256 values are g (tbl8 group gidx): inline when it can be
+// (and allow_inline; 0 keeps every group in tbl8, for A/B measurements).
+INFW_TD uint64_t infw_d24_encode(const uint32_t *g, uint32_t gidx, bool allow_inline = true) {
+    uint32_t v[3] = {g[0], 0, 0}, b[2] = {0, 0}, runs = 1;
+    bool ok = allow_inline && g[0] <= INFW_D24_MAXV;
+    for (uint32_t x = 1; x < 256 && ok; x++) {
+        if (g[x] == g[x - 1]) continue;
+        if (runs == 3 || g[x] > INFW_D24_MAXV) ok = false;
+        else {
+            b[runs - 1] = x;
+            v[runs++] = g[x];
+        }
+    }
+    if (!ok) return INFW_D24_GROUP | gidx;
+    if (runs == 1) return g[0];
+    if (runs == 2) {
+        v[2] = v[1];
+        b[1] = b[0];
+    }
+    return INFW_D24_GROUP | INFW_D24_INLINE | (uint64_t)b[1] << 53 | (uint64_t)b[0] << 45 | (uint64_t)v[2] << 30 |
+           (uint64_t)v[1] << 15 | v[0];
+}
+
+INFW_TD uint32_t infw_d24_inline(uint64_t e, uint32_t x) {
+    const uint32_t b1 = (uint32_t)(e >> 45) & 0xFFu, b2 = (uint32_t)(e >> 53) & 0xFFu;
+    const uint32_t sh = x >= b2 ? 30u : x >= b1 ? 15u : 0u;
+    return (uint32_t)(e >> sh) & INFW_D24_MAXV;
+}
+
 template <class T>
 INFW_TD uint32_t infw_dir24_lookup(const T &t, uint32_t slot, uint32_t a32) {
-    uint32_t e = t.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
-    if (e & INFW_TBL8_FLAG) e = t.tbl8[((uint64_t)(e & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu)];
-    return e;
+    const uint64_t e = t.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+    if (!(e & INFW_D24_GROUP)) return (uint32_t)e;
+    if (e & INFW_D24_INLINE) return infw_d24_inline(e, a32 & 0xFFu);
+    return t.tbl8[((uint64_t)(uint32_t)e << 8) | (a32 & 0xFFu)];
 }
 
 template <class T>

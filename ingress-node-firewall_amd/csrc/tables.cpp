@@ -529,8 +529,9 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         return a.slot != b.slot ? a.slot < b.slot : a.plen < b.plen;
     });
     out.short_mode = short_mode_req >= 0 ? (uint32_t)short_mode_req
-                     : ((uint64_t)out.n_slots << 26) <= dir24_budget ? INFW_SHORT_DIR24 : INFW_SHORT_COMPRESSED;
+                     : ((uint64_t)out.n_slots << 27) <= dir24_budget ? INFW_SHORT_DIR24 : INFW_SHORT_COMPRESSED;
     const bool dir24 = out.short_mode == INFW_SHORT_DIR24;
+    if (const char *e = getenv("INFW_D24_INLINE")) out.d24_inline = atoi(e) != 0;
     out.l16.assign(dir24 ? 1 : (size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
     {
         std::vector<uint32_t> t24, t8;
@@ -585,11 +586,17 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             out.n_tbl8_groups += t8.size() >> 8;
             if (dir24) {  // keep the DIR-24-8 image as the device form
-                if (out.tbl24.empty()) out.tbl24.assign((size_t)out.n_slots << 24, 0u);
+                if (out.tbl24.empty()) out.tbl24.assign((size_t)out.n_slots << 24, 0ull);
                 const uint32_t gbase = (uint32_t)(out.tbl8.size() >> 8);
                 for (size_t k = 0; k < ((size_t)1 << 24); k++) {
-                    uint32_t w = t24[k];
-                    out.tbl24[((size_t)slot << 24) + k] = (w & INFW_TBL8_FLAG) ? (INFW_TBL8_FLAG | (gbase + (w & ~INFW_TBL8_FLAG))) : w;
+                    const uint32_t w = t24[k];
+                    if (w & INFW_TBL8_FLAG) {
+                        const uint32_t lg = w & ~INFW_TBL8_FLAG;
+                        out.tbl24[((size_t)slot << 24) + k] = infw_d24_encode(&t8[(size_t)lg << 8], gbase + lg, out.d24_inline);
+                        out.tbl8_of[(uint64_t)slot << 24 | k] = gbase + lg;
+                    } else {
+                        out.tbl24[((size_t)slot << 24) + k] = w;
+                    }
                 }
                 out.tbl8.insert(out.tbl8.end(), t8.begin(), t8.end());
                 si = sj;

@@ -83,8 +83,32 @@ static int run_case(int n_keys, int v4_share, int max_rules, int mode, int seed)
     return 0;
 }
 
-int main() {
+// DIR-24-8 word encoding: every 256-value /24 pattern decodes to itself, inline or via its group.
+static int check_d24_words() {
+    static uint32_t tbl8[256];
+    struct {
+        const uint32_t *tbl8;
+        const uint64_t *tbl24;
+    } t{tbl8, nullptr};
     int bad = 0;
+    for (int c = 0; c < 20000; c++) {
+        const uint32_t runs = 1 + rnd() % 5, big = c % 7 == 0 ? 0x8000u : 0u;
+        uint32_t x = 0;
+        for (uint32_t r = 0; r < runs; r++) {
+            const uint32_t v = (rnd() % 0x8000u) | (r == 1 ? big : 0u), end = r + 1 == runs ? 256 : x + rnd() % (257 - x);
+            for (; x < end; x++) tbl8[x] = v;
+        }
+        const uint64_t w = infw_d24_encode(tbl8, 0);
+        t.tbl24 = &w;
+        for (uint32_t a = 0; a < 256; a++) bad |= infw_dir24_lookup(t, 0, a) != tbl8[a];
+        bad |= (runs <= 3 && !big) && (w & INFW_D24_GROUP) && !(w & INFW_D24_INLINE) && tbl8[0] != tbl8[255];
+    }
+    if (bad) printf("d24 word encoding mismatch\n");
+    return bad;
+}
+
+int main() {
+    int bad = check_d24_words();
     const int modes[3] = {INFW_SHORT_DIR24, INFW_SHORT_COMPRESSED, -1};
     for (int s = 0; s < 3; s++)
         for (int mi = 0; mi < 3; mi++) {

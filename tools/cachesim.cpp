@@ -9,7 +9,7 @@
 // ("current"; INFW_DT_PARTS / INFW_DT_FORM select it) and for candidate layouts
 // expressed as alternative address maps over the single-part layout
 // (INFW_DT_PARTS=1):
-//   tbl24_u16   DIR-24-8 words of 2 bytes
+//   tbl24_u16   DIR-24-8 words of 2 bytes (no inline /24s)
 //   entry32     decision entries of 32 B, a list's classes packed in 128-B lines
 //   quartersQ / partsQxB   entry lines addressed by (list, class, value part)
 // Build + run: make cachesim   (tools/cachesim [n_packets])
@@ -117,6 +117,45 @@ int main(int argc, char **argv) {
         printf("{\"parts\": %d, \"lines\": %llu, \"over_20_segments\": %llu}\n", Q, (unsigned long long)parts,
                (unsigned long long)over);
     }
+    {  // path census (compiled layout): which lookups a packet needs
+        uint64_t v4 = 0, v4_8 = 0, v6 = 0, v6_long = 0, v6_short = 0, v6_8 = 0, nolist = 0;
+        std::vector<uint32_t> runs_hist(9, 0);
+        for (uint64_t g = 0; g < (h.tbl8.size() >> 8); g++) {
+            uint32_t r = 1;
+            for (int j = 1; j < 256; j++) r += h.tbl8[g * 256 + j] != h.tbl8[g * 256 + j - 1];
+            runs_hist[r < 8 ? r : 8]++;
+        }
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            const int pk = infw_parse(q[6], q[7], &cls, &val);
+            if (pk < INFW_PK_V4) continue;
+            const int slot = infw_if_slot(t, q[4]);
+            if (slot < 0) continue;
+            const uint32_t a32 = infw_bswap32(q[0]);
+            const uint64_t w = t.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+            const bool grp = (w & INFW_D24_GROUP) && !(w & INFW_D24_INLINE);
+            if (pk == INFW_PK_V4) {
+                v4++;
+                v4_8 += grp;
+            } else {
+                v6++;
+                if (infw_v6_long(t, (uint32_t)slot, a32, q)) v6_long++;
+                else {
+                    v6_short++;
+                    v6_8 += grp;
+                }
+            }
+            nolist += infw_lpm(t, pk, q[4], q) == 0;
+        }
+        printf("{\"census\": {\"v4\": %.4f, \"v4_tbl8\": %.4f, \"v6\": %.4f, \"v6_long_hit\": %.4f, "
+               "\"v6_then_short\": %.4f, \"v6_tbl8\": %.4f, \"no_entry\": %.4f}, \"tbl8_runs_hist\": [",
+               (double)v4 / n, (double)v4_8 / n, (double)v6 / n, (double)v6_long / n, (double)v6_short / n,
+               (double)v6_8 / n, (double)nolist / n);
+        for (int r = 0; r < 9; r++) printf("%s%u", r ? ", " : "", runs_hist[r]);
+        printf("]}\n");
+    }
     for (const Variant &V : vars) {
         std::vector<L2> l2(8, L2(4ull << 20));
         uint64_t req[S_N] = {}, miss[S_N] = {};
@@ -140,14 +179,13 @@ int main(int argc, char **argv) {
                 }
                 if (!lng) {
                     const uint64_t w = ((uint64_t)slot << 24) | (a32 >> 8);
-                    tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 4)};
-                    uint32_t e = t.tbl24[w];
-                    if (e & INFW_TBL8_FLAG) {
-                        const uint64_t w8 = ((uint64_t)(e & ~INFW_TBL8_FLAG) << 8) | (a32 & 0xFFu);
-                        tc[nt++] = {S_TBL8, 2 * kSpace + w8 * (V.tbl24_u16 ? 2 : 4)};
-                        e = t.tbl8[w8];
+                    tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 8)};
+                    const uint64_t e = t.tbl24[w];
+                    if ((e & INFW_D24_GROUP) && !(e & INFW_D24_INLINE)) {
+                        const uint64_t w8 = ((uint64_t)(uint32_t)e << 8) | (a32 & 0xFFu);
+                        tc[nt++] = {S_TBL8, 2 * kSpace + w8 * 4};
                     }
-                    l1 = e;
+                    l1 = infw_dir24_lookup(t, (uint32_t)slot, a32);
                 } else {
                     l1 = lng;
                 }
