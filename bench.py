@@ -130,12 +130,14 @@ def main():
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
 
     traffic = None
+    traffic_from = None
     line_model = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_packet", None)
             traffic = None if traffic is None else round(traffic * n)
+            traffic_from = f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this command)"
             # random-line model: the kernel's PMC L2 hits/misses per packet priced at the
             # chip's measured random-lookup rates; frac = that bound / the measured kernel time
             r = tj.get("line_rates")
@@ -180,6 +182,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
+            "traffic_from": traffic_from,
             "kernel": "classify_kernel<512, 0>",
             "kernel_ms_avg": round(avg_kern_ms, 4),
             "algorithmic_bytes_per_packet": ALGO_BYTES_PER_PKT,

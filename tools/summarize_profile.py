@@ -56,9 +56,12 @@ def main():
         out["hbm_bytes_per_launch"] = corr
         out["hbm_bytes_per_packet"] = corr / n
         out["hbm_bytes_per_packet_raw"] = raw / n
-        json.dump({"tag": tag, "hbm_bytes_per_packet": corr / n, "hbm_bytes_per_packet_raw": raw / n,
-                   "note": "classify kernel, cfg2 bench config; see profiles/%s/summary.json" % tag},
-                  open(os.path.join(ROOT, "profiles", "traffic_cfg2.json"), "w"), indent=1)
+        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+        tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        keep = {k: tj[k] for k in ("line_rates",) if k in tj}  # microbenchmark rates outlive a profile
+        json.dump(dict({"tag": tag, "hbm_bytes_per_packet": corr / n, "hbm_bytes_per_packet_raw": raw / n,
+                        "note": "classify kernel, cfg2 bench config; see profiles/%s/summary.json" % tag}, **keep),
+                  open(tp, "w"), indent=1)
     if "TCC_HIT_sum" in avg:
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         out["l2_misses_per_packet"] = avg["TCC_MISS_sum"] / n
