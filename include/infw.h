@@ -265,6 +265,22 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, ui
                      uint32_t *result_words, uint8_t *xdp_verdicts,
                      const struct infw_classify_ex *ex, void *stream);
 
+/* Host-resident batch: the SoA streams, result words and verdicts live in   */
+/* host memory (as a cgo caller hands them over).  The batch goes through    */
+/* the device in chunks of `chunk` packets (0 = 4M) with three HIP streams:  */
+/* the H2D copy of chunk k+1 and the D2H copy of chunk k-1 overlap the       */
+/* kernel on chunk k; two sets of chunk buffers per device are owned by the  */
+/* context.  The whole batch reads one table epoch.  Synchronous: returns    */
+/* when every result is in host memory.  Full PCIe rate needs pinned or      */
+/* registered host memory (hipHostMalloc / infw_host_register); pageable     */
+/* memory is correct but staged by the HIP runtime.  Statistics accumulate   */
+/* in the device's slot exactly as for infw_classify.                         */
+int infw_classify_host(infw_ctx *ctx, int dev, const struct infw_batch_soa *host_in, uint64_t n,
+                       uint32_t *host_results, uint8_t *host_verdicts, uint64_t chunk);
+/* Page-lock (hipHostRegister) / release a host range for infw_classify_host. */
+int infw_host_register(infw_ctx *ctx, void *ptr, uint64_t bytes);
+int infw_host_unregister(infw_ctx *ctx, void *ptr);
+
 /* ------------------------------------------------------------------------ */
 /* Statistics — ingress_node_firewall_statistics_map (kernel.c:36-41,        */
 /* PERCPU_ARRAY[1024] of ruleStatistics_st).  One slot per device plays the  */

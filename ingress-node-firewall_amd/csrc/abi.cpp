@@ -91,6 +91,35 @@ struct Device {
     uint64_t *dbg_fp = nullptr;
     uint32_t *dbg_keys = nullptr;
     uint32_t *dbg_count = nullptr;
+    std::shared_ptr<struct HostPipe> pipe;  // infw_classify_host chunk buffers + streams
+};
+
+// Two chunk slots of device buffers and three streams for host-resident batches.
+struct HostPipe {
+    int ordinal = -1;
+    uint64_t chunk = 0;
+    hipStream_t h2d = nullptr, run = nullptr, d2h = nullptr;
+    struct Slot {
+        uint8_t *saddr = nullptr;
+        uint32_t *ifindex = nullptr, *pkt_len = nullptr, *meta = nullptr, *l4word = nullptr, *res = nullptr;
+        uint8_t *ver = nullptr;
+        hipEvent_t in_done = nullptr, run_done = nullptr, out_done = nullptr;
+    } slot[2];
+    std::mutex mu;
+    ~HostPipe() {
+        if (ordinal < 0) return;
+        DeviceGuard g(ordinal);
+        (void)hipDeviceSynchronize();
+        for (auto &s : slot) {
+            for (void *p : {(void *)s.saddr, (void *)s.ifindex, (void *)s.pkt_len, (void *)s.meta, (void *)s.l4word,
+                            (void *)s.res, (void *)s.ver})
+                if (p) (void)hipFree(p);
+            for (hipEvent_t e : {s.in_done, s.run_done, s.out_done})
+                if (e) (void)hipEventDestroy(e);
+        }
+        for (hipStream_t st : {h2d, run, d2h})
+            if (st) (void)hipStreamDestroy(st);
+    }
 };
 
 constexpr uint32_t kDbgSlots = 2 * INFW_DBG_MAX_ENTRIES;
@@ -330,7 +359,9 @@ int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_
 void infw_destroy(infw_ctx *ctx) {
     if (!ctx) return;
     for (auto &d : ctx->devs) {
+        d.pipe.reset();
         d.epoch.reset();
+        d.spare.reset();
         DeviceGuard g(d.ordinal);
         (void)hipDeviceSynchronize();
         if (d.stats_own) (void)hipFree(d.stats_own);
@@ -574,6 +605,108 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
+    return 0;
+}
+
+static int make_pipe(int ordinal, uint64_t chunk, std::shared_ptr<HostPipe> &out) {
+    DeviceGuard g(ordinal);
+    if (!g.ok) return -ENODEV;
+    auto p = std::make_shared<HostPipe>();
+    p->ordinal = ordinal;
+    p->chunk = chunk;
+    HIP_OK(hipStreamCreateWithFlags(&p->h2d, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&p->run, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&p->d2h, hipStreamNonBlocking));
+    for (auto &s : p->slot) {
+        HIP_OK(hipMalloc(&s.saddr, chunk * 16));
+        HIP_OK(hipMalloc(&s.ifindex, chunk * 4));
+        HIP_OK(hipMalloc(&s.pkt_len, chunk * 4));
+        HIP_OK(hipMalloc(&s.meta, chunk * 4));
+        HIP_OK(hipMalloc(&s.l4word, chunk * 4));
+        HIP_OK(hipMalloc(&s.res, chunk * 4));
+        HIP_OK(hipMalloc(&s.ver, chunk));
+        HIP_OK(hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&s.run_done, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&s.out_done, hipEventDisableTiming));
+    }
+    out = p;
+    return 0;
+}
+
+int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n, uint32_t *results,
+                       uint8_t *verdicts, uint64_t chunk) {
+    if (!ctx || !in) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("classify_host: host-only context has no device tables");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (n && (!in->saddr || !in->ifindex || !in->pkt_len || !in->meta || !in->l4word)) {
+        set_error("classify_host: null input stream");
+        return -EINVAL;
+    }
+    if (n == 0) return 0;
+    chunk = chunk ? chunk : (4u << 20);
+    chunk = (chunk + 511) & ~511ull;  // whole tiles
+    Device &d = ctx->devs[dev];
+    std::shared_ptr<HostPipe> pipe;
+    {
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        pipe = d.pipe;
+    }
+    if (!pipe || pipe->chunk != chunk) {
+        int rc = make_pipe(d.ordinal, chunk, pipe);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        d.pipe = pipe;
+    }
+    std::lock_guard<std::mutex> plk(pipe->mu);  // one host batch at a time per device
+    std::shared_ptr<DeviceEpoch> ep;             // the whole batch reads one epoch
+    {
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        ep = d.epoch;
+    }
+    DeviceGuard g(d.ordinal);
+    if (!g.ok) return -ENODEV;
+    const uint64_t nchunks = (n + chunk - 1) / chunk;
+    for (uint64_t k = 0; k < nchunks; k++) {
+        HostPipe::Slot &s = pipe->slot[k & 1];
+        const uint64_t a = k * chunk, c = std::min(chunk, n - a);
+        // the slot's buffers are free once chunk k-2's results left the device
+        HIP_OK(hipStreamWaitEvent(pipe->h2d, s.out_done, 0));
+        HIP_OK(hipMemcpyAsync(s.saddr, in->saddr + 16 * a, c * 16, hipMemcpyHostToDevice, pipe->h2d));
+        HIP_OK(hipMemcpyAsync(s.ifindex, in->ifindex + a, c * 4, hipMemcpyHostToDevice, pipe->h2d));
+        HIP_OK(hipMemcpyAsync(s.pkt_len, in->pkt_len + a, c * 4, hipMemcpyHostToDevice, pipe->h2d));
+        HIP_OK(hipMemcpyAsync(s.meta, in->meta + a, c * 4, hipMemcpyHostToDevice, pipe->h2d));
+        HIP_OK(hipMemcpyAsync(s.l4word, in->l4word + a, c * 4, hipMemcpyHostToDevice, pipe->h2d));
+        HIP_OK(hipEventRecord(s.in_done, pipe->h2d));
+        HIP_OK(hipStreamWaitEvent(pipe->run, s.in_done, 0));
+        const infw_batch_soa db{s.saddr, s.ifindex, s.pkt_len, s.meta, s.l4word};
+        if (infw_launch_classify(&ep->view, &db, c, results ? s.res : nullptr, verdicts ? s.ver : nullptr, d.stats,
+                                 d.cus, ctx->block, ctx->group, ctx->blocks_per_cu, pipe->run, nullptr, 0, nullptr,
+                                 ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots)) {
+            set_error(std::string("classify_host launch failed: ") + hipGetErrorString(hipGetLastError()));
+            return -EIO;
+        }
+        HIP_OK(hipEventRecord(s.run_done, pipe->run));
+        HIP_OK(hipStreamWaitEvent(pipe->d2h, s.run_done, 0));
+        if (results) HIP_OK(hipMemcpyAsync(results + a, s.res, c * 4, hipMemcpyDeviceToHost, pipe->d2h));
+        if (verdicts) HIP_OK(hipMemcpyAsync(verdicts + a, s.ver, c, hipMemcpyDeviceToHost, pipe->d2h));
+        HIP_OK(hipEventRecord(s.out_done, pipe->d2h));
+    }
+    HIP_OK(hipStreamSynchronize(pipe->d2h));
+    return 0;
+}
+
+int infw_host_register(infw_ctx *ctx, void *ptr, uint64_t bytes) {
+    if (!ctx || !ptr || !bytes) return -EINVAL;
+    HIP_OK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return 0;
+}
+
+int infw_host_unregister(infw_ctx *ctx, void *ptr) {
+    if (!ctx || !ptr) return -EINVAL;
+    HIP_OK(hipHostUnregister(ptr));
     return 0;
 }
 

@@ -122,7 +122,8 @@ ABI_SYMBOLS = [
     "infw_table_commit", "infw_classify", "infw_stats_read", "infw_stats_read_all", "infw_stats_reset",
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
-    "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear",
+    "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
+    "infw_host_register", "infw_host_unregister",
 ]
 
 
@@ -161,6 +162,10 @@ _sig = {
     "infw_classify_ex": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
                                    P(ClassifyEx), C.c_void_p]),
     "infw_pack_frames": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoa), C.c_void_p]),
+    "infw_classify_host": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
+                                     C.c_uint64]),
+    "infw_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "infw_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "infw_stats_read": (C.c_int, [C.c_void_p, C.c_uint32, P(RuleStatisticsSt), P(C.c_int)]),
     "infw_stats_read_all": (C.c_int, [C.c_void_p, P(RuleStatisticsSt)]),
     "infw_stats_reset": (C.c_int, [C.c_void_p]),

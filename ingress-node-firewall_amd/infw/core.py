@@ -174,6 +174,23 @@ class Classifier:
                                      verdicts.data_ptr() if verdicts is not None else None, C.byref(ex), sp),
               "classify_ex")
 
+    def classify_host(self, soa: "HostSoa", results=None, verdicts=None, dev: int = 0, chunk: int = 0) -> None:
+        """Host-resident batch (numpy arrays, see HostSoa): pipelined through the device in chunks; returns when
+        results (uint32 array) / verdicts (uint8 array) are filled."""
+        b = N.BatchSoa(soa.saddr.ctypes.data, soa.ifindex.ctypes.data, soa.pkt_len.ctypes.data,
+                       soa.meta.ctypes.data, soa.l4word.ctypes.data)
+        check(N.lib.infw_classify_host(self._ctx, dev, C.byref(b), soa.n,
+                                       results.ctypes.data if results is not None else None,
+                                       verdicts.ctypes.data if verdicts is not None else None, chunk),
+              "classify_host")
+
+    def host_register(self, arr: np.ndarray) -> None:
+        """Page-lock a numpy array's memory for full-rate infw_classify_host copies."""
+        check(N.lib.infw_host_register(self._ctx, arr.ctypes.data, arr.nbytes), "host_register")
+
+    def host_unregister(self, arr: np.ndarray) -> None:
+        check(N.lib.infw_host_unregister(self._ctx, arr.ctypes.data), "host_unregister")
+
     def pack_frames(self, frames, linear_len, ifindex, out, pkt_len=None, offsets=None, stride: int = 0,
                     dev: int = 0, stream=None) -> None:
         """Frames in device memory (uint8 tensor) -> the SoA batch `out` on the device (§8f-3)."""
@@ -238,6 +255,29 @@ class Classifier:
         out = np.zeros(t.shape[0], dtype=np.uint32)
         check(N.lib.infw_debug_walk(self._ctx, t.ctypes.data, t.shape[0], out.ctypes.data), "debug_walk")
         return out
+
+
+class HostSoa:
+    """struct infw_batch_soa in host memory: five numpy streams (saddr n x 16 u8, ifindex, pkt_len, meta, l4word)."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.saddr = np.zeros((n, 16), np.uint8)
+        self.ifindex = np.zeros(n, np.uint32)
+        self.pkt_len = np.zeros(n, np.uint32)
+        self.meta = np.zeros(n, np.uint32)
+        self.l4word = np.zeros(n, np.uint32)
+
+    @staticmethod
+    def from_tuples(t: np.ndarray) -> "HostSoa":
+        """t: n x 8 u32 tuples {saddr[4], ifindex, pkt_len, meta, l4word}."""
+        h = HostSoa(t.shape[0])
+        h.saddr[:] = np.ascontiguousarray(t[:, :4]).view(np.uint8).reshape(-1, 16)
+        h.ifindex[:], h.pkt_len[:], h.meta[:], h.l4word[:] = t[:, 4], t[:, 5], t[:, 6], t[:, 7]
+        return h
+
+    def arrays(self):
+        return (self.saddr, self.ifindex, self.pkt_len, self.meta, self.l4word)
 
 
 def verdicts_from_results(results: np.ndarray, meta: np.ndarray) -> np.ndarray:

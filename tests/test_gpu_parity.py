@@ -386,3 +386,31 @@ def test_incremental_commits_on_device():
         if info["commit_mode"] == infw.COMMIT_INCREMENTAL:
             assert info["patch_bytes"] < (8 << 20), info["patch_bytes"]
     assert modes.count(infw.COMMIT_INCREMENTAL) >= 4 and infw.COMMIT_REUPLOAD in modes, modes
+
+
+def test_classify_host_batches():
+    """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
+    pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    n = 300001
+    hdr, cap, pl, ifx = wl.frames(0, n)
+    ores, over, ost, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    soa = infw.HostSoa.from_tuples(wl.tuples(0, n))
+    for chunk, pin in ((65536, False), (1 << 22, True)):
+        if pin:
+            for a in soa.arrays():
+                clf.host_register(a)
+        res = np.zeros(n, np.uint32)
+        ver = np.zeros(n, np.uint8)
+        clf.stats_reset()
+        clf.classify_host(soa, res, ver, chunk=chunk)
+        assert np.array_equal(res, ores), chunk
+        assert np.array_equal(ver, over), chunk
+        assert np.array_equal(clf.stats_read_all(), ost), chunk
+        if pin:
+            for a in soa.arrays():
+                clf.host_unregister(a)
