@@ -156,6 +156,28 @@ int main(int argc, char **argv) {
         for (int r = 0; r < 9; r++) printf("%s%u", r ? ", " : "", runs_hist[r]);
         printf("]}\n");
     }
+    for (int lds_entries : {256, 1024, 2048}) {  // per-workgroup direct-mapped LDS cache of tbl24 words
+        const uint32_t wgs = (uint32_t)(n / 131072) ? (uint32_t)(n / 131072) : 1;  // ~131k packets per workgroup, as at 128M packets over 1024 workgroups
+        std::vector<uint64_t> tag((size_t)wgs * lds_entries, ~0ull);
+        uint64_t look = 0, hit = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            const int pk = infw_parse(q[6], q[7], &cls, &val);
+            if (pk != INFW_PK_V4) continue;
+            const int slot = infw_if_slot(t, q[4]);
+            if (slot < 0) continue;
+            const uint64_t key = ((uint64_t)slot << 24) | (infw_bswap32(q[0]) >> 8);
+            const uint32_t wg = (uint32_t)((i / 512) % wgs);
+            uint64_t &e = tag[(size_t)wg * lds_entries + (key * 0x9E3779B1u >> 8) % lds_entries];
+            look++;
+            if (e == key) hit++;
+            else e = key;
+        }
+        printf("{\"lds_tbl24_cache\": %d, \"v4_lookups_per_packet\": %.4f, \"hit_rate\": %.4f}\n", lds_entries,
+               (double)look / n, (double)hit / look);
+    }
     for (const Variant &V : vars) {
         std::vector<L2> l2(8, L2(4ull << 20));
         uint64_t req[S_N] = {}, miss[S_N] = {};
