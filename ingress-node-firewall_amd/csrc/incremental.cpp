@@ -14,7 +14,7 @@
 //                    class records) — lists are only appended, never moved.
 // Everything that would change the layout — a new ifindex, the compressed
 // short table, a group crossing 3 records (the Waldvogel overflow table), the
-// first long prefix, a bucket table past half load, too many edits, or half of
+// first long prefix, a bucket table past 1/4 load, too many edits, or half of
 // the lists unreferenced — is left to a full compile.  Decisions are made
 // before anything is modified, so "needs a full compile" leaves the image intact.
 #include <errno.h>
@@ -146,7 +146,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (e.now) rv.push_back(infw_v6_rec{e.lo, mid, (e.P - 32) << 25});  // list filled in pass 2
         if (rv.size() > INFW_BUCKET_INLINE) return full("IPv6 group exceeds 3 prefixes");
     }
-    if ((h.n_buckets + new_buckets) * 2 > h.btab.size()) return full("IPv6 bucket table past half load");
+    // compiled at load <= 1/8; past 1/4 the probe chains a wave waits for grow: recompile
+    if ((h.n_buckets + new_buckets) * 4 > h.btab.size()) return full("IPv6 bucket table past 1/4 load");
     // two new groups may share an insert position: they must not
     {
         std::vector<uint64_t> pos;

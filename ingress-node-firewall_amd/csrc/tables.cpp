@@ -706,8 +706,12 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             g.recs.push_back(infw_v6_rec{r.lo, (uint32_t)r.hi, (r.len - 32) << 25 | r.list1});
         }
+        // a wave waits for its slowest lane's probe chain: keep the load at or below 1/8
+        // (INFW_BUCKET_SPREAD=k: capacity >= k x groups), the untouched capacity costs no cache
+        uint64_t spread = 8;
+        if (const char *e = getenv("INFW_BUCKET_SPREAD")) spread = std::max(2, atoi(e));
         uint64_t cap = 1024;
-        while (cap < groups.size() * 2) cap <<= 1;
+        while (cap < groups.size() * spread) cap <<= 1;
         out.btab.assign(cap, infw_v6_bucket{});
         memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
         const uint64_t bmask = cap - 1;

@@ -156,6 +156,40 @@ int main(int argc, char **argv) {
         for (int r = 0; r < 9; r++) printf("%s%u", r ? ", " : "", runs_hist[r]);
         printf("]}\n");
     }
+    {  // IPv6 bucket probe lengths: per lookup, and the slowest lane of each 64-packet wave
+        uint64_t looks = 0, probes = 0, waves = 0, wave_max_sum = 0;
+        uint32_t hist[8] = {};
+        uint32_t wmax = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            if (i % 64 == 0 && i) {
+                wave_max_sum += wmax;
+                waves++;
+                wmax = 0;
+            }
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            if (infw_parse(q[6], q[7], &cls, &val) != INFW_PK_V6 || !t.n_levels) continue;
+            const int slot = infw_if_slot(t, q[4]);
+            if (slot < 0) continue;
+            const uint32_t a32 = infw_bswap32(q[0]);
+            uint64_t b = infw_bucket_hash((uint32_t)slot, a32) & t.bmask;
+            uint32_t np = 1;
+            for (;;) {
+                const infw_v6_bucket &bk = t.btab[b];
+                if (bk.tag == 0 || (bk.tag == (uint32_t)slot + 1 && bk.top == a32)) break;
+                b = (b + 1) & t.bmask;
+                np++;
+            }
+            looks++;
+            probes += np;
+            hist[np < 8 ? np : 7]++;
+            wmax = np > wmax ? np : wmax;
+        }
+        printf("{\"v6_bucket_probes\": %.3f, \"wave_max_probes\": %.3f, \"load\": %.3f, \"hist\": [%u, %u, %u, %u, %u, %u, %u]}\n",
+               (double)probes / looks, (double)wave_max_sum / waves, (double)h.n_buckets / h.btab.size(), hist[1],
+               hist[2], hist[3], hist[4], hist[5], hist[6], hist[7]);
+    }
     for (int lds_entries : {256, 1024, 2048}) {  // per-workgroup direct-mapped LDS cache of tbl24 words
         const uint32_t wgs = (uint32_t)(n / 131072) ? (uint32_t)(n / 131072) : 1;  // ~131k packets per workgroup, as at 128M packets over 1024 workgroups
         std::vector<uint64_t> tag((size_t)wgs * lds_entries, ~0ull);
