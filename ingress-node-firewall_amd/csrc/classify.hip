@@ -123,6 +123,32 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
     return r;
 }
 
+// Longest /33../128 prefix covering an IPv6 address (infw_v6_long, device form):
+// each probe reads the whole 64-B bucket — header and the three records — in one
+// round of loads, so a lane's probe costs one dependent L2 round trip, not one
+// for the header and one per record examined.
+__device__ __forceinline__ uint32_t v6_long_dev(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
+                                                const uint32_t sa[4]) {
+    const uint32_t mid = infw_bswap32(sa[1]);
+    const uint64_t lo = infw_be64(sa[2], sa[3]);
+    uint64_t i = infw_bucket_hash(slot, a32) & T.bmask;
+    for (;;) {
+        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + i);
+        const u32x4 h = b[0], r0 = b[1], r1 = b[2], r2 = b[3];
+        if (h[0] == 0) return 0;
+        if (h[0] == slot + 1 && h[1] == a32) {
+            const uint32_t nb = h[2];
+            if (nb == INFW_BUCKET_OVERFLOW) return infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
+            // infw_v6_rec {lo u64, mid, meta}: words 0-1, 2, 3; longest record first
+            if (nb >= 1 && infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
+            if (nb >= 2 && infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo)) return r1[3] & 0x1FFFFFFu;
+            if (nb >= 3 && infw_rec_match(r2[2], (uint64_t)r2[1] << 32 | r2[0], r2[3], mid, lo)) return r2[3] & 0x1FFFFFFu;
+            return 0;
+        }
+        i = (i + 1) & T.bmask;
+    }
+}
+
 // G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
 struct EventSink {
     infw_event_rec *rec;
@@ -292,7 +318,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     uint32_t lng = 0, sh = 0;
                     // diagnostic 64: fetch the short table beside the IPv6 bucket (speculative)
                     if (kAblate & 64) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
-                    if (pk == INFW_PK_V6 && T.n_levels) lng = infw_v6_long(T, (uint32_t)slot, a32, sw);
+                    if (pk == INFW_PK_V6 && T.n_levels)
+                        lng = (kAblate & 256) ? infw_v6_long(T, (uint32_t)slot, a32, sw)  // diagnostic 256: header-first form
+                                              : v6_long_dev(T, (uint32_t)slot, a32, sw);
                     if (!(kAblate & 64) && !lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 }
@@ -454,6 +482,7 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 32: launch<512, 0, 32>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 256: launch<512, 0, 256>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         }
