@@ -38,6 +38,13 @@ constexpr uint32_t kC24 = 1024;   // per-workgroup LDS cache of plain DIR-24-8 w
 // list+1} written and read whole, so lanes racing on a slot can only replace
 // one complete entry by another: a hit is always the table's own word.  Only
 // plain words are cached; inline /24s and tbl8 groups take the table path.
+// Decode a DIR-24-8 word for address a32 (tbl8 only for a /24 with > 3 runs).
+__device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t w, uint32_t a32) {
+    if (!(w & INFW_D24_GROUP)) return (uint32_t)w;
+    if (w & INFW_D24_INLINE) return infw_d24_inline(w, a32 & 0xFFu);
+    return T.tbl8[((uint64_t)(uint32_t)w << 8) | (a32 & 0xFFu)];
+}
+
 template <bool kCache>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                         unsigned long long *s_c24) {
@@ -127,6 +134,34 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
 // each probe reads the whole 64-B bucket — header and the three records — in one
 // round of loads, so a lane's probe costs one dependent L2 round trip, not one
 // for the header and one per record examined.
+// Finish a first bucket probe whose header h and first record r0 are already loaded:
+// most groups hold one record, so records 1..2 (and further probes) load on demand.
+__device__ __forceinline__ uint32_t v6_finish(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
+                                             const uint32_t sa[4], uint64_t i, u32x4 h, u32x4 r0) {
+    const uint32_t mid = infw_bswap32(sa[1]);
+    const uint64_t lo = infw_be64(sa[2], sa[3]);
+    for (;;) {
+        if (h[0] == 0) return 0;
+        if (h[0] == slot + 1 && h[1] == a32) {
+            const uint32_t nb = h[2];
+            if (nb == INFW_BUCKET_OVERFLOW) return infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
+            if (nb >= 1 && infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
+            if (nb >= 2) {
+                const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + i);
+                const u32x4 r1 = b[2], r2 = b[3];
+                if (infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo)) return r1[3] & 0x1FFFFFFu;
+                if (nb >= 3 && infw_rec_match(r2[2], (uint64_t)r2[1] << 32 | r2[0], r2[3], mid, lo))
+                    return r2[3] & 0x1FFFFFFu;
+            }
+            return 0;
+        }
+        i = (i + 1) & T.bmask;
+        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + i);
+        h = b[0];
+        r0 = b[1];
+    }
+}
+
 __device__ __forceinline__ uint32_t v6_long_dev(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                 const uint32_t sa[4]) {
     const uint32_t mid = infw_bswap32(sa[1]);
@@ -310,18 +345,51 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     slot = infw_if_slot(T, ifx);
                 }
                 l1 = 0;
-                if (slot >= 0) {
+                if (slot >= 0 && !(kAblate & 512)) {
+                    // One round of table loads for the whole wave: IPv4 lanes' DIR-24-8 words
+                    // and IPv6 lanes' first bucket probe are issued before either is waited
+                    // for (a mixed wave would otherwise pay two dependent round trips).  IPv6:
+                    // the /32 group's bucket; the short table only when no long prefix covers
+                    // the address (2.8 % of them at configs[2]).
                     const uint32_t a32 = infw_bswap32(sa.x);
-                    // IPv6: the /32 group's bucket first; the short table only when no
-                    // long prefix covers the address (the kernel is bound by random
-                    // memory traffic, not latency: no speculative short-table fetch)
+                    const bool v6 = pk == INFW_PK_V6 && T.n_levels;
+                    const bool d24 = T.short_mode == INFW_SHORT_DIR24;
+                    const uint32_t key = (uint32_t)slot << 24 | a32 >> 8;
+                    const uint32_t cidx = (key * 0x9E3779B1u) >> 22;
+                    bool need24 = !v6 && d24;
+                    uint32_t sh = 0;
+                    if (kCache && need24 && slot < 256) {
+                        const unsigned long long e = s_c24[cidx];
+                        if ((e >> 63) && (uint32_t)(e >> 31) == key) {
+                            sh = (uint32_t)e & 0x7FFFFFFFu;
+                            need24 = false;
+                        }
+                    }
+                    uint64_t w24 = 0, bi = 0;
+                    u32x4 bh = {0, 0, 0, 0}, br0 = {0, 0, 0, 0};
+                    if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+                    if (v6) {
+                        bi = infw_bucket_hash((uint32_t)slot, a32) & T.bmask;
+                        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
+                        bh = b[0];
+                        br0 = b[1];
+                    }
+                    uint32_t lng = 0;
+                    if (v6) lng = v6_finish(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                    if (need24) {
+                        sh = d24_value(T, w24, a32);
+                        if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
+                            s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
+                    } else if (!v6 && !d24) {
+                        sh = infw_short_lookup(T, (uint32_t)slot, a32);  // compressed / no short table
+                    }
+                    if (v6 && !lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
+                    l1 = lng ? lng : sh;
+                } else if (slot >= 0) {  // diagnostic 512: the sequential form (bucket round, then tbl24 round)
+                    const uint32_t a32 = infw_bswap32(sa.x);
                     uint32_t lng = 0, sh = 0;
-                    // diagnostic 64: fetch the short table beside the IPv6 bucket (speculative)
-                    if (kAblate & 64) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
-                    if (pk == INFW_PK_V6 && T.n_levels)
-                        lng = (kAblate & 256) ? infw_v6_long(T, (uint32_t)slot, a32, sw)  // diagnostic 256: header-first form
-                                              : v6_long_dev(T, (uint32_t)slot, a32, sw);
-                    if (!(kAblate & 64) && !lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
+                    if (pk == INFW_PK_V6 && T.n_levels) lng = v6_long_dev(T, (uint32_t)slot, a32, sw);
+                    if (!lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 }
             }
@@ -482,7 +550,7 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 32: launch<512, 0, 32>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 256: launch<512, 0, 256>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+        case 512: launch<512, 0, 512>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
         }
