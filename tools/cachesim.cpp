@@ -15,8 +15,11 @@
 // Build + run: make cachesim   (tools/cachesim [n_packets])
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../ingress-node-firewall_amd/csrc/infw_internal.h"
@@ -67,6 +70,8 @@ struct Variant {
     int quarters;  // > 0: decision lines addressed by (list, class, value >> (16 - log2 quarters))
     int slot_bytes = 64;  // bytes per (list, class, part) slot: a compact leaf of 20 / 10 / 5 segments
     int entry_stride = 64;
+    int dense_short = 0;  // 1: short-table lookups touch one 8-B word per matched prefix, prefixes sorted by (slot, address)
+    int pairing = 0;  // 1: compiled parts, entry line at ((list * 16 + part) * 8 + cls) * 64 (classes of one part adjacent)
 };
 
 }  // namespace
@@ -98,12 +103,29 @@ int main(int argc, char **argv) {
             step_function(recs, st, rs);
             seg_starts[(size_t)l * INFW_NCLS + c] = st;
         }
+    // short-table prefixes (<= 32 address bits) ranked by (slot, address, length)
+    std::unordered_map<uint64_t, uint64_t> short_rank;
+    {
+        std::vector<std::pair<uint64_t, uint64_t>> v;  // ((slot, net), L) -> key
+        for (uint64_t i = 0; i < ne; i++) {
+            const uint32_t L = keys[i].prefixLen - 32;
+            if (L > 32) continue;
+            const int sl = infw_if_slot(t, keys[i].ingress_ifindex);
+            if (sl < 0) continue;
+            uint32_t a = (uint32_t)keys[i].ip_data[0] << 24 | keys[i].ip_data[1] << 16 | keys[i].ip_data[2] << 8 | keys[i].ip_data[3];
+            a = L ? a & (~0u << (32 - L)) : 0;
+            v.push_back({((uint64_t)sl << 32 | a) << 6 | L, ((uint64_t)sl << 40) | ((uint64_t)L << 32) | a});
+        }
+        std::sort(v.begin(), v.end());
+        for (uint64_t r = 0; r < v.size(); r++) short_rank[v[r].second] = r;
+    }
     const Variant vars[] = {{"current", false, false, 0}, {"tbl24_u16", true, false, 0}, {"entry32", false, true, 0},
                             {"quarters4", false, false, 4}, {"quarters8", false, false, 8},
                             {"quarters16", false, false, 16}, {"parts16x32B", false, false, 16, 32},
                             {"parts32x32B", false, false, 32, 32}, {"parts32x16B", false, false, 32, 16},
                             {"parts64x16B", false, false, 64, 16}, {"parts8x32B", false, false, 8, 32},
-                            {"stride128", false, false, 0, 64, 128}};
+                            {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 1},
+                            {"dense_short", false, false, 0, 64, 64, 1}};
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -212,7 +234,46 @@ int main(int argc, char **argv) {
         printf("{\"lds_tbl24_cache\": %d, \"v4_lookups_per_packet\": %.4f, \"hit_rate\": %.4f}\n", lds_entries,
                (double)look / n, (double)hit / look);
     }
+    // per-workgroup direct-mapped LDS caches of whole 64-B lines: decision entry lines keyed by
+    // (list, class, part) and IPv6 first-probe bucket lines keyed by (slot, /32)
+    for (int lines : {64, 128, 256, 512}) {
+        const uint32_t wgs = (uint32_t)(n / 131072) ? (uint32_t)(n / 131072) : 1;
+        std::vector<uint64_t> etag((size_t)wgs * lines, ~0ull), btag((size_t)wgs * lines, ~0ull);
+        uint64_t el = 0, eh = 0, bl = 0, bh = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            const int pk = infw_parse(q[6], q[7], &cls, &val);
+            if (pk < INFW_PK_V4) continue;
+            const int slot = infw_if_slot(t, q[4]);
+            if (slot < 0) continue;
+            const uint32_t wg = (uint32_t)((i / 512) % wgs);
+            const uint32_t a32 = infw_bswap32(q[0]);
+            if (pk == INFW_PK_V6 && t.n_levels) {
+                const uint64_t key = ((uint64_t)slot << 32) | a32;
+                uint64_t &e = btag[(size_t)wg * lines + ((key * 0x9E3779B97F4A7C15ull) >> 40) % lines];
+                bl++;
+                if (e == key) bh++;
+                else e = key;
+            }
+            const uint32_t l1 = infw_lpm(t, pk, q[4], q);
+            if (!l1) continue;
+            const uint64_t key = infw_dt_slot(l1 - 1, cls, val, t.dt_plog2);
+            uint64_t &e = etag[(size_t)wg * lines + ((key * 0x9E3779B97F4A7C15ull) >> 40) % lines];
+            el++;
+            if (e == key) eh++;
+            else e = key;
+        }
+        printf("{\"lds_line_cache\": %d, \"entry_lookups_per_packet\": %.4f, \"entry_hit_rate\": %.4f, "
+               "\"bucket_lookups_per_packet\": %.4f, \"bucket_hit_rate\": %.4f}\n",
+               lines, (double)el / n, (double)eh / el, (double)bl / n, (double)bh / bl);
+        fflush(stdout);
+    }
+    if (getenv("CACHESIM_LDS_ONLY")) return 0;
+    const char *only = getenv("CACHESIM_VARIANTS");
     for (const Variant &V : vars) {
+        if (only && !strstr(only, V.name)) continue;
         std::vector<L2> l2(8, L2(4ull << 20));
         uint64_t req[S_N] = {}, miss[S_N] = {};
         for (uint64_t i = 0; i < n; i++) {
@@ -236,6 +297,15 @@ int main(int argc, char **argv) {
                 if (!lng) {
                     const uint64_t w = ((uint64_t)slot << 24) | (a32 >> 8);
                     tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 8)};
+                    if (V.dense_short) {  // the longest <= /32 prefix covering a32 in this slot
+                        uint64_t r = ~0ull;
+                        for (int L = 32; L >= 0 && r == ~0ull; L--) {
+                            const uint32_t net = L ? a32 & (~0u << (32 - L)) : 0;
+                            auto it = short_rank.find(((uint64_t)slot << 40) | ((uint64_t)L << 32) | net);
+                            if (it != short_rank.end()) r = it->second;
+                        }
+                        tc[nt - 1].addr = 1 * kSpace + (r == ~0ull ? (1ull << 35) + w * 8 : r * 8);
+                    }
                     const uint64_t e = t.tbl24[w];
                     if ((e & INFW_D24_GROUP) && !(e & INFW_D24_INLINE)) {
                         const uint64_t w8 = ((uint64_t)(uint32_t)e << 8) | (a32 & 0xFFu);
@@ -266,6 +336,8 @@ int main(int argc, char **argv) {
                 tc[nt++] = {S_ENTRY, 3 * kSpace + (V.entry32 ? (uint64_t)(l1 - 1) * 256 + cls * 32 : ei * V.entry_stride)};
                 const uint64_t slot_i = infw_dt_slot(l1 - 1, cls, val, t.dt_plog2);
                 if (t.dt_plog2) tc[nt - 1].addr = 3 * kSpace + slot_i * 64;  // the compiled layout's entry line
+                if (t.dt_plog2 && V.pairing)
+                    tc[nt - 1].addr = 3 * kSpace + (((uint64_t)(l1 - 1) * 16 + (val >> 12)) * 8 + cls) * 64;
                 const uint32_t *w = t.dte[slot_i].w;
                 if (w[0] & INFW_DT_ROOT) {
                     const uint64_t li = (w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, val);
