@@ -132,6 +132,7 @@ def main():
     traffic = None
     traffic_from = None
     line_model = None
+    extra = {}
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -148,6 +149,14 @@ def main():
                               "hit_rate_G_per_s": r["l2_hit_G_per_s"], "miss_rate_G_per_s": r["l2_miss_G_per_s"],
                               "bound_ms": round(bound_ms, 3), "frac": round(bound_ms / avg_kern_ms, 3),
                               "counters_from": tj.get("tag")}
+            # SURVEY.md §8d's side figures: fabric-side line traffic (one TCC_EA0_RDREQ per 128-B line, stream and
+            # gathers alike) as GB/s at this run's kernel time, and the LDS bank-conflict rate
+            if "ea_rdreq_per_packet" in tj:
+                extra["line_traffic_GBps_at_128B"] = round(tj["ea_rdreq_per_packet"] * 128 * n / (avg_kern_ms * 1e-3)
+                                                           / 1e9, 1)
+                extra["fetch_size_GBps"] = round(traffic / (avg_kern_ms * 1e-3) / 1e9, 1) if traffic else None
+            if "lds_bank_conflict_rate" in tj:
+                extra["lds_bank_conflict_rate"] = round(tj["lds_bank_conflict_rate"], 4)
         except Exception:
             traffic = None
 
@@ -187,6 +196,7 @@ def main():
             "kernel_ms_avg": round(avg_kern_ms, 4),
             "algorithmic_bytes_per_packet": ALGO_BYTES_PER_PKT,
             "random_line_model": line_model,
+            **extra,
         },
         "cpu_baseline": None,
     }
@@ -213,12 +223,15 @@ def cpu_baseline(args, wl, results, n):
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     # bounded sample, in chunks of 8M frame snapshots (80 B each) so host memory stays ~0.7 GB;
     # only the oracle's classify calls are timed (frame synthesis is not CPU-path work)
-    secs, parity, chunk = 0.0, True, 8 << 20
+    secs, parity, chunk, examined, ex_n = 0.0, True, 8 << 20, 0, 0
     for off in range(0, s, chunk):
         c = min(chunk, s - off)
         hdr, cap, pl, ifx = wl.frames(off, c)
         res, _, _, dt = m.classify_frames(hdr, cap, pl, ifx, nthreads=threads)
         secs += dt
+        if off == 0:  # the reference's scan work on the first 1M packets (single thread, not timed)
+            ex_n = min(c, 1 << 20)
+            examined = m.rules_examined(hdr[:ex_n], cap[:ex_n], pl[:ex_n], ifx[:ex_n])
         gpu = results[off:off + c].cpu().numpy().view(np.uint32)
         parity = parity and bool(np.array_equal(gpu, res))
         del hdr, cap, pl, ifx, res
@@ -230,6 +243,9 @@ def cpu_baseline(args, wl, results, n):
         "sample": f"first {s} packets of rank 0's cfg{args.cfg} batch, {threads} pthreads, oracle/infw_oracle.c "
                   f"(frame parse + hash-per-length LPM + 100-slot scan), {secs:.2f}s of classify wall time",
         "gpu_results_bitexact_on_sample": parity,
+        # bytes of rule records the reference's in-order loop examines per packet (12 B per valid
+        # rule up to and including the first match); the GPU path reads one 64-B decision line instead
+        "reference_rule_bytes_examined_per_packet": round(12 * examined / max(ex_n, 1), 2),
     }
 
 

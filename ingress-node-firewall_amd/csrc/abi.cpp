@@ -3,6 +3,7 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -70,12 +71,93 @@ struct DeviceEpoch {
     infw_dev_tables view;
     uint64_t bytes = 0;
     std::vector<DirtyRange> pending;
+    // The last classify launch on this image per stream.  An incremental commit orders its
+    // upload into this image (while it is the spare) after exactly these launches — on the
+    // device, through its patch stream — and records `ready` behind the upload; launches on
+    // the image once it is live wait for `ready` in their own stream.  Neither the host nor
+    // the batch running on the live image waits for the other.
+    std::mutex use_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    bool use_overflow = false;  // more streams than tracked: the host waits for the device instead
+    hipEvent_t ready = nullptr;
+    bool ready_armed = false;
+    void mark_use(hipStream_t s) {
+        std::lock_guard<std::mutex> lk(use_mu);
+        hipEvent_t ev = nullptr;
+        for (auto &u : uses)
+            if (u.first == s) ev = u.second;
+        if (!ev) {
+            if (uses.size() >= 32 || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                use_overflow = true;
+                return;
+            }
+            uses.emplace_back(s, ev);
+        }
+        if (hipEventRecord(ev, s) != hipSuccess) use_overflow = true;
+    }
+    // make stream `ps` wait for every launch that read this image
+    int order_after_uses(hipStream_t ps) {
+        std::lock_guard<std::mutex> lk(use_mu);
+        DeviceGuard g(ordinal);
+        if (use_overflow) {
+            use_overflow = false;
+            return hipDeviceSynchronize() == hipSuccess ? 0 : -EIO;
+        }
+        for (auto &u : uses)
+            if (hipStreamWaitEvent(ps, u.second, 0) != hipSuccess) return -EIO;
+        return 0;
+    }
+    // a launch on this image, on stream s, starts after the image's last upload
+    int wait_ready(hipStream_t s) {
+        if (!ready_armed) return 0;
+        return hipStreamWaitEvent(s, ready, 0) == hipSuccess ? 0 : -EIO;
+    }
     ~DeviceEpoch() {
         if (ordinal < 0) return;
         DeviceGuard g(ordinal);
         (void)hipDeviceSynchronize();  // batches launched on this image have finished
         for (void *p : buf)
             if (p) (void)hipFree(p);
+        for (auto &u : uses) (void)hipEventDestroy(u.second);
+        if (ready) (void)hipEventDestroy(ready);
+    }
+};
+
+// Incremental-commit upload path of one device: a non-blocking stream (never ordered
+// behind classify launches on the null or any blocking stream) and pinned host + device
+// staging buffers, grown on demand and kept.
+struct PatchPipe {
+    int ordinal = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *host = nullptr, *dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;  // the last upload out of the staging buffers
+    bool done_armed = false;
+    int reserve(size_t bytes) {
+        if (done_armed) {  // the previous commit's upload has left the staging buffers
+            if (hipEventSynchronize(done) != hipSuccess) return -EIO;
+            done_armed = false;
+        }
+        if (bytes <= cap) return 0;
+        size_t c = cap ? cap : (1u << 20);
+        while (c < bytes) c *= 2;
+        if (host) (void)hipHostFree(host);
+        if (dev) (void)hipFree(dev);
+        host = dev = nullptr;
+        cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&host), c, hipHostMallocDefault) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(reinterpret_cast<void **>(&dev), c) != hipSuccess) return -ENOMEM;
+        cap = c;
+        return 0;
+    }
+    ~PatchPipe() {
+        if (ordinal < 0) return;
+        DeviceGuard g(ordinal);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (done) (void)hipEventDestroy(done);
+        if (host) (void)hipHostFree(host);
+        if (dev) (void)hipFree(dev);
+        if (stream) (void)hipStreamDestroy(stream);
     }
 };
 
@@ -92,6 +174,7 @@ struct Device {
     uint32_t *dbg_keys = nullptr;
     uint32_t *dbg_count = nullptr;
     std::shared_ptr<struct HostPipe> pipe;  // infw_classify_host chunk buffers + streams
+    std::shared_ptr<PatchPipe> patch;       // incremental-commit uploads
 };
 
 // Two chunk slots of device buffers and three streams for host-resident batches.
@@ -228,10 +311,16 @@ static bool image_fits(const DeviceEpoch &ep, const HostTables &h) {
     return true;
 }
 
-// Copy ep.pending (merged) from the host image into the device image: small
-// sets range by range, larger ones as one staging upload + one scatter launch.
-static int flush_pending(DeviceEpoch &ep, const HostTables &h, uint32_t cus, uint64_t *bytes_out) {
+// Copy ep.pending (merged, widened to whole words) from the host image into the
+// device image through the device's non-blocking patch stream, asynchronously: the
+// caller has ordered the stream after the image's last readers; ep.ready marks the end.
+static int flush_pending(DeviceEpoch &ep, const HostTables &h, uint32_t cus, PatchPipe &pp, uint64_t *bytes_out) {
     std::vector<DirtyRange> &r = ep.pending;
+    for (DirtyRange &x : r) {  // whole 4-B words (every table buffer is an array of >= 4-B elements)
+        const uint64_t end = (x.off + x.len + 3) & ~3ull;
+        x.off &= ~3ull;
+        x.len = end - x.off;
+    }
     std::sort(r.begin(), r.end(), [](const DirtyRange &a, const DirtyRange &b) {
         return a.buf != b.buf ? a.buf < b.buf : a.off < b.off;
     });
@@ -245,41 +334,59 @@ static int flush_pending(DeviceEpoch &ep, const HostTables &h, uint32_t cus, uin
     }
     r.clear();
     DeviceGuard g(ep.ordinal);
+    struct Piece {
+        const uint8_t *src;
+        uint8_t *dst;
+        uint64_t len;
+    };
+    std::vector<Piece> pieces;
     uint64_t total = 0;
-    std::vector<uint32_t> staging;
-    std::vector<infw_patch_desc> descs;
     for (const DirtyRange &x : m) {
         const void *p;
         size_t bytes;
         host_buffer(h, (int)x.buf, &p, &bytes);
-        const uint64_t len = std::min<uint64_t>(x.len, bytes > x.off ? bytes - x.off : 0);
+        const uint64_t len = std::min<uint64_t>(x.len, bytes > x.off ? (bytes - x.off) & ~3ull : 0);
         if (!len) continue;
+        pieces.push_back({static_cast<const uint8_t *>(p) + x.off, static_cast<uint8_t *>(ep.buf[x.buf]) + x.off, len});
         total += len;
-        const uint8_t *src = static_cast<const uint8_t *>(p) + x.off;
-        uint8_t *dst = static_cast<uint8_t *>(ep.buf[x.buf]) + x.off;
-        if (m.size() <= 16) {
-            HIP_OK(hipMemcpy(dst, src, len, hipMemcpyHostToDevice));
-            continue;
-        }
-        descs.push_back(infw_patch_desc{(uint64_t)(uintptr_t)dst, (uint64_t)staging.size(), len / 4});
-        staging.insert(staging.end(), reinterpret_cast<const uint32_t *>(src),
-                       reinterpret_cast<const uint32_t *>(src) + len / 4);
     }
-    if (!descs.empty()) {
-        void *ds = nullptr, *dd = nullptr;
-        HIP_OK(hipMalloc(&ds, staging.size() * 4));
-        HIP_OK(hipMalloc(&dd, descs.size() * sizeof(infw_patch_desc)));
-        int rc = 0;
-        if (hipMemcpy(ds, staging.data(), staging.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(dd, descs.data(), descs.size() * sizeof(infw_patch_desc), hipMemcpyHostToDevice) != hipSuccess ||
-            infw_launch_scatter(static_cast<const uint32_t *>(ds), dd, (uint32_t)descs.size(), cus, nullptr) ||
-            hipDeviceSynchronize() != hipSuccess) {
-            set_error(std::string("table patch upload failed: ") + hipGetErrorString(hipGetLastError()));
-            rc = -EIO;
+    if (!pieces.empty()) {
+        const size_t dbytes = (pieces.size() * sizeof(infw_patch_desc) + 255) & ~(size_t)255;
+        int rc = pp.reserve(dbytes + total);
+        if (rc) {
+            set_error("table patch: staging allocation failed");
+            return rc;
         }
-        (void)hipFree(ds);
-        (void)hipFree(dd);
-        if (rc) return rc;
+        auto *descs = reinterpret_cast<infw_patch_desc *>(pp.host);
+        uint8_t *words = pp.host + dbytes;
+        uint64_t w = 0;
+        for (size_t i = 0; i < pieces.size(); i++) {
+            memcpy(words + 4 * w, pieces[i].src, pieces[i].len);
+            descs[i] = infw_patch_desc{(uint64_t)(uintptr_t)pieces[i].dst, w, pieces[i].len / 4};
+            w += pieces[i].len / 4;
+        }
+        // few ranges: DMA copies straight from the pinned staging (no compute unit needed, so they
+        // proceed while a classify launch occupies every CU); many: one upload + one scatter launch
+        bool ok = true;
+        if (pieces.size() <= 64) {
+            for (size_t i = 0; i < pieces.size() && ok; i++)
+                ok = hipMemcpyAsync(pieces[i].dst, words + 4 * descs[i].src, pieces[i].len, hipMemcpyHostToDevice,
+                                    pp.stream) == hipSuccess;
+        } else {
+            ok = hipMemcpyAsync(pp.dev, pp.host, dbytes + total, hipMemcpyHostToDevice, pp.stream) == hipSuccess &&
+                 !infw_launch_scatter(reinterpret_cast<const uint32_t *>(pp.dev + dbytes), pp.dev,
+                                      (uint32_t)pieces.size(), cus, pp.stream);
+        }
+        if (ok && !ep.ready) ok = hipEventCreateWithFlags(&ep.ready, hipEventDisableTiming) == hipSuccess;
+        if (ok && !pp.done) ok = hipEventCreateWithFlags(&pp.done, hipEventDisableTiming) == hipSuccess;
+        if (ok) ok = hipEventRecord(ep.ready, pp.stream) == hipSuccess && hipEventRecord(pp.done, pp.stream) == hipSuccess;
+        if (!ok) {
+            set_error(std::string("table patch upload failed: ") + hipGetErrorString(hipGetLastError()));
+            (void)hipStreamSynchronize(pp.stream);
+            return -EIO;
+        }
+        ep.ready_armed = true;
+        pp.done_armed = true;
     }
     if (bytes_out) *bytes_out += total;
     return 0;
@@ -360,6 +467,7 @@ void infw_destroy(infw_ctx *ctx) {
     if (!ctx) return;
     for (auto &d : ctx->devs) {
         d.pipe.reset();
+        d.patch.reset();
         d.epoch.reset();
         d.spare.reset();
         DeviceGuard g(d.ordinal);
@@ -464,13 +572,26 @@ int infw_table_commit(infw_ctx *ctx) {
             if (d.spare && image_fits(*d.spare, h)) {
                 // batches that took the spare while it was live have launched and finished
                 while (d.spare.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
-                {
-                    DeviceGuard g(d.ordinal);
-                    HIP_OK(hipDeviceSynchronize());
-                }
                 next = d.spare;
+                if (!d.patch) {
+                    DeviceGuard g(d.ordinal);
+                    auto pp = std::make_shared<PatchPipe>();
+                    pp->ordinal = d.ordinal;
+                    HIP_OK(hipStreamCreateWithFlags(&pp->stream, hipStreamNonBlocking));
+                    d.patch = pp;
+                }
+                const auto w0 = std::chrono::steady_clock::now();
+                rc = next->order_after_uses(d.patch->stream);  // after the batches that read this image
+                const auto w1 = std::chrono::steady_clock::now();
                 next->pending.insert(next->pending.end(), ranges.begin(), ranges.end());
-                rc = flush_pending(*next, h, d.cus, &patched);
+                if (!rc) rc = flush_pending(*next, h, d.cus, *d.patch, &patched);
+                if (getenv("INFW_COMMIT_TRACE"))
+                    fprintf(stderr, "[commit] patch %.3f ms, order %.3f ms, stage %.3f ms, %zu ranges\n",
+                            std::chrono::duration<double, std::milli>(w0 - t1).count() +
+                                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                            std::chrono::duration<double, std::milli>(w1 - w0).count(),
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w1).count(),
+                            ranges.size());
                 if (rc) {
                     std::lock_guard<std::mutex> lk(ctx->epoch_mu);
                     d.spare.reset();  // half-patched: never used again
@@ -597,6 +718,10 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
         return -ENODEV;
     }
     const bool evs = ex && ex->events_count;
+    if (ep->wait_ready(static_cast<hipStream_t>(stream))) {
+        set_error("classify: stream wait on the epoch's upload failed");
+        return -EIO;
+    }
     int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.cus, ctx->block,
                                   ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream),
                                   evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr,
@@ -605,6 +730,7 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
+    ep->mark_use(static_cast<hipStream_t>(stream));
     return 0;
 }
 
@@ -668,6 +794,7 @@ int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_
     }
     DeviceGuard g(d.ordinal);
     if (!g.ok) return -ENODEV;
+    HIP_OK(ep->wait_ready(pipe->run) ? hipErrorUnknown : hipSuccess);
     const uint64_t nchunks = (n + chunk - 1) / chunk;
     for (uint64_t k = 0; k < nchunks; k++) {
         HostPipe::Slot &s = pipe->slot[k & 1];
@@ -694,6 +821,7 @@ int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_
         if (verdicts) HIP_OK(hipMemcpyAsync(verdicts + a, s.ver, c, hipMemcpyDeviceToHost, pipe->d2h));
         HIP_OK(hipEventRecord(s.out_done, pipe->d2h));
     }
+    ep->mark_use(pipe->run);
     HIP_OK(hipStreamSynchronize(pipe->d2h));
     return 0;
 }

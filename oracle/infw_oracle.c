@@ -337,8 +337,10 @@ static inline uint16_t bpf_ntohs(uint16_t x) { return (uint16_t)((x >> 8) | (x <
 /* The first-match loop shared by ipv4_firewall_lookup (:222-258) and
  * ipv6_firewall_lookup (:306-340); they differ only in the ICMP protocol
  * number honoured (IPPROTO_ICMP on the v4 path, IPPROTO_ICMPV6 on v6). */
+/* examined (may be NULL): += the valid rules (ruleId != 0) looked at, up to and
+ * including the first match (SURVEY.md §8d "rule bytes examined" = 12 B each). */
 static uint32_t scan_rules(const uint8_t *rulesVal, uint8_t proto, uint16_t dstPort,
-                           uint8_t icmpType, uint8_t icmpCode, uint8_t icmp_proto) {
+                           uint8_t icmpType, uint8_t icmpCode, uint8_t icmp_proto, uint64_t *examined) {
     for (int i = 0; i < ORC_MAX_RULES; ++i) {
         const uint8_t *r = rulesVal + 12 * i;
         uint32_t ruleId = rd_le32(r);
@@ -347,6 +349,7 @@ static uint32_t scan_rules(const uint8_t *rulesVal, uint8_t proto, uint16_t dstP
         uint16_t dstPortEnd = rd_le16(r + 7);
         uint8_t rIcmpType = r[9], rIcmpCode = r[10], action = r[11];
         if (ruleId == INVALID_RULE_ID) continue;
+        if (examined) ++*examined;
         if (protocol != 0 && protocol == proto) {
             if (protocol == IPPROTO_TCP || protocol == IPPROTO_UDP || protocol == IPPROTO_SCTP) {
                 if (dstPortEnd == 0) {
@@ -369,7 +372,7 @@ static uint32_t scan_rules(const uint8_t *rulesVal, uint8_t proto, uint16_t dstP
 
 /* ipv4_firewall_lookup, kernel.c:189-262 */
 static uint32_t ipv4_firewall_lookup(const orc_map *m, const uint8_t *data, uint32_t data_end,
-                                     uint32_t ifId) {
+                                     uint32_t ifId, uint64_t *examined) {
     uint16_t dstPort = 0;
     uint8_t icmpCode = 0, icmpType = 0, proto = 0;
     if (ip_extract_l4info(data, data_end, &proto, &dstPort, &icmpType, &icmpCode, 1) < 0)
@@ -379,12 +382,12 @@ static uint32_t ipv4_firewall_lookup(const orc_map *m, const uint8_t *data, uint
     memcpy(kd + 4, data + ETH_HLEN + 12, 4);          /* key.ip_data[0..3] = saddr bytes */
     const map_ent *e = map_lpm(m, 64, kd);            /* key.prefixLen = 64 (:207) */
     if (!e) return SET_ACTION(UNDEF);
-    return scan_rules(e->val, proto, dstPort, icmpType, icmpCode, IPPROTO_ICMP);
+    return scan_rules(e->val, proto, dstPort, icmpType, icmpCode, IPPROTO_ICMP, examined);
 }
 
 /* ipv6_firewall_lookup, kernel.c:277-344 */
 static uint32_t ipv6_firewall_lookup(const orc_map *m, const uint8_t *data, uint32_t data_end,
-                                     uint32_t ifId) {
+                                     uint32_t ifId, uint64_t *examined) {
     uint16_t dstPort = 0;
     uint8_t icmpCode = 0, icmpType = 0, proto = 0;
     if (ip_extract_l4info(data, data_end, &proto, &dstPort, &icmpType, &icmpCode, 0) < 0)
@@ -394,7 +397,7 @@ static uint32_t ipv6_firewall_lookup(const orc_map *m, const uint8_t *data, uint
     memcpy(kd + 4, data + ETH_HLEN + 8, 16);          /* iph->saddr */
     const map_ent *e = map_lpm(m, 160, kd);           /* key.prefixLen = 160 (:293) */
     if (!e) return SET_ACTION(UNDEF);
-    return scan_rules(e->val, proto, dstPort, icmpType, icmpCode, IPPROTO_ICMPV6);
+    return scan_rules(e->val, proto, dstPort, icmpType, icmpCode, IPPROTO_ICMPV6, examined);
 }
 
 /* generate_event_and_update_statistics, kernel.c:361-400 (statistics part;
@@ -416,17 +419,17 @@ static void update_statistics(struct orc_stats *stats, uint64_t packet_len, uint
 }
 
 /* ingress_node_firewall_main, kernel.c:412-457 */
-int orc_xdp_run(const orc_map *m, struct orc_stats *stats, const uint8_t *data,
-                uint32_t linear_len, uint32_t buff_len, uint32_t ifindex, uint32_t *result_out,
-                int *event_out) {
+static int xdp_run(const orc_map *m, struct orc_stats *stats, const uint8_t *data, uint32_t linear_len,
+                   uint32_t buff_len, uint32_t ifindex, uint32_t *result_out, int *event_out,
+                   uint64_t *examined) {
     uint32_t result = UNDEF;
     if (result_out) *result_out = 0;
     if (event_out) *event_out = 0;
     if (ETH_HLEN > linear_len) return XDP_DROP;       /* :423-426 */
     uint16_t h_proto = (uint16_t)(data[12] << 8 | data[13]);
     switch (h_proto) {
-    case 0x0800: result = ipv4_firewall_lookup(m, data, linear_len, ifindex); break;
-    case 0x86DD: result = ipv6_firewall_lookup(m, data, linear_len, ifindex); break;
+    case 0x0800: result = ipv4_firewall_lookup(m, data, linear_len, ifindex, examined); break;
+    case 0x86DD: result = ipv6_firewall_lookup(m, data, linear_len, ifindex, examined); break;
     default: return XDP_PASS;                         /* :436-438 */
     }
     if (result_out) *result_out = result;
@@ -443,6 +446,24 @@ int orc_xdp_run(const orc_map *m, struct orc_stats *stats, const uint8_t *data,
     default:
         return XDP_PASS;
     }
+}
+
+int orc_xdp_run(const orc_map *m, struct orc_stats *stats, const uint8_t *data,
+                uint32_t linear_len, uint32_t buff_len, uint32_t ifindex, uint32_t *result_out,
+                int *event_out) {
+    return xdp_run(m, stats, data, linear_len, buff_len, ifindex, result_out, event_out, NULL);
+}
+
+uint64_t orc_rules_examined(const orc_map *m, const uint8_t *frames, const uint64_t *offsets,
+                            const uint32_t *caplen, const uint32_t *pkt_len, const uint32_t *ifindex,
+                            uint64_t n) {
+    uint64_t ex = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t lin = caplen[i] < pkt_len[i] ? caplen[i] : pkt_len[i];
+        uint32_t res;
+        xdp_run(m, NULL, frames + offsets[i], lin, pkt_len[i], ifindex[i], &res, NULL, &ex);
+    }
+    return ex;
 }
 
 /* ------------------------------------------------------------------------ */

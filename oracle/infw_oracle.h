@@ -87,6 +87,12 @@ double orc_classify_frames(const orc_map *m, const uint8_t *frames, const uint64
                            const uint32_t *ifindex, uint64_t n, uint32_t *results,
                            uint8_t *verdicts, struct orc_stats *stats_sum, int nthreads);
 
+/* Valid rules (ruleId != 0) the reference's first-match loop examines over a batch,
+ * up to and including each packet's first match (x 12 B = rule bytes). */
+uint64_t orc_rules_examined(const orc_map *m, const uint8_t *frames, const uint64_t *offsets,
+                            const uint32_t *caplen, const uint32_t *pkt_len, const uint32_t *ifindex,
+                            uint64_t n);
+
 /* Events of a batch: fills up to max_events DENY events in packet order. */
 uint64_t orc_collect_events(const orc_map *m, const uint8_t *frames, const uint64_t *offsets,
                             const uint32_t *caplen, const uint32_t *pkt_len,

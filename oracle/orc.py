@@ -31,6 +31,8 @@ _sig = {
                               P(C.c_uint32), P(C.c_int)]),
     "orc_classify_frames": (C.c_double, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "orc_rules_examined": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_uint64]),
     "orc_collect_events": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
     "orc_collect_lookup_keys": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -120,6 +122,20 @@ class OracleMap:
                                         None if res is None else res.ctypes.data,
                                         None if ver is None else ver.ctypes.data, stats.ctypes.data, nthreads)
         return res, ver, stats, secs
+
+    def rules_examined(self, hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifindex: np.ndarray) -> int:
+        """Valid rules the reference's first-match loop looks at over the batch, up to and including each
+        packet's first match (rule bytes examined = 12 B each)."""
+        n = hdr.shape[0]
+        h = np.ascontiguousarray(hdr, dtype=np.uint8)
+        w = h.shape[1] if n else 0
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(w)
+        cap = np.ascontiguousarray(caplen, np.uint32)
+        cap = cap if w >= 80 else np.minimum(cap, np.uint32(max(w, 0)))
+        pl = np.ascontiguousarray(pkt_len, np.uint32)
+        ifx = np.ascontiguousarray(ifindex, np.uint32)
+        return int(_lib.orc_rules_examined(self._m, h.ctypes.data, offs.ctypes.data, cap.ctypes.data,
+                                           pl.ctypes.data, ifx.ctypes.data, n))
 
     def collect_events(self, hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifindex: np.ndarray,
                        max_events: int | None = None):

@@ -181,6 +181,25 @@ def test_demo1_sample():
         assert (a, r) == (act, res), (src, proto, port)
 
 
+def test_rules_examined_oracle():
+    """SURVEY.md §8d "rule bytes examined": valid rules the in-order loop looks at, up to and including the match
+    (kernel.c:222-258); ruleId-0 slots are skipped and not counted, a lookup miss or a parse failure examines none."""
+    from frames import snapshots
+    m = orc.OracleMap()
+    rules = [{"order": 1, "protocol": "TCP", "ports": "100-200", "action": "Allow"},
+             {"order": 5, "protocol": "UDP", "ports": 53, "action": "Allow"},
+             {"order": 10, "protocol": "", "action": "Deny"}]
+    assert m.update(goenc.build_key(1, "10.0.0.0/8"), goenc.make_value(rules)) == 0
+    cases = [(frame("10.1.2.3", proto="tcp", dport=150), 1), (frame("10.1.2.3", proto="udp", dport=53), 2),
+             (frame("10.1.2.3", proto="icmp"), 3), (frame("10.1.2.3", proto="tcp", dport=7), 3),
+             (frame("11.1.2.3", proto="tcp", dport=150), 0), (frame("10.1.2.3", proto="gre"), 0)]
+    for f, want in cases:
+        hdr, cap, pl = snapshots([f])
+        assert m.rules_examined(hdr, cap, pl, np.array([1], np.uint32)) == want
+    hdr, cap, pl = snapshots([f for f, _ in cases])
+    assert m.rules_examined(hdr, cap, pl, np.ones(len(cases), np.uint32)) == sum(w for _, w in cases)
+
+
 def test_debug_lookup_keys_oracle():
     """The dbg-map key of each probe packet (kernel.c:205-216, :291-299): only packets whose L4 header was
     extracted insert; IPv4 keys are {64, ifindex, saddr, 12 zero bytes}, IPv6 keys {160, ifindex, saddr}."""

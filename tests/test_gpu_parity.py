@@ -388,6 +388,58 @@ def test_incremental_commits_on_device():
     assert modes.count(infw.COMMIT_INCREMENTAL) >= 4 and infw.COMMIT_REUPLOAD in modes, modes
 
 
+def test_commits_while_batches_in_flight():
+    """configs[4] live swap with the device busy: batch A is queued on a side stream (repeated, so it is
+    still running), then two incremental commits are made before A finishes and batch B is classified on
+    the second new epoch.  Incremental commits patch only the spare image and wait only for the launches
+    that read it, so A (on epoch 1) must equal the oracle's epoch 1 and B the oracle's epoch 3."""
+    import random
+    import orc
+    from test_incremental_cpu import _apply
+    wl = W.Workload(W.CFG4_ADVERSARIAL, n_prefixes=20000, n_templates=64)
+    ents = list(wl.entries())
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)
+    m1 = orc.OracleMap(max_entries=wl.n_entries + 4096)
+    for k, v in ents:
+        _apply((clf,), m1, k, v)
+    clf.commit()
+    dev = torch.device("cuda", 0)
+    n = 1 << 20
+    a, b = SoaBatch.empty(n, dev), SoaBatch.empty(n, dev)
+    wl.gen_device(a, 0, 0)
+    wl.gen_device(b, n, 0)
+    torch.cuda.synchronize()
+    rng = random.Random(5)
+    vals = [v for _, v in ents]
+    edits = [[(k, None if rng.random() < 0.25 else rng.choice(vals)) for k, _ in rng.sample(ents, 300)]
+             for _ in range(2)]
+    m3 = orc.OracleMap(max_entries=wl.n_entries + 4096)
+    for k, v in ents:
+        m3.update(k, v)
+    for k, v in edits[0]:  # staged: classify keeps reading epoch 1 until the commit
+        _apply((clf,), m3, k, v)
+    side = torch.cuda.Stream(dev)
+    res_a = torch.empty(n, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(side):
+        for _ in range(400):  # >10 ms of work queued on epoch 1
+            clf.classify(a, results=res_a, stream=side)
+    clf.commit()  # patches the spare; A keeps running on epoch 1
+    assert clf.info()["commit_mode"] == infw.COMMIT_INCREMENTAL
+    for k, v in edits[1]:
+        _apply((clf,), m3, k, v)
+    clf.commit()  # the spare is now epoch 1's image: this one waits for A's launches
+    assert clf.info()["commit_mode"] == infw.COMMIT_INCREMENTAL
+    gres_b, _ = gpu_run(clf, b, n)
+    side.synchronize()
+    hdr, cap, pl, ifx = wl.frames(0, n)
+    want_a, _, _, _ = m1.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(res_a.cpu().numpy().view(np.uint32), want_a)
+    hdr, cap, pl, ifx = wl.frames(n, n)
+    want_b, _, _, _ = m3.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(gres_b, want_b)
+    assert not np.array_equal(want_a, m3.classify_frames(*wl.frames(0, n), nthreads=8)[0])  # the edits matter
+
+
 def test_classify_host_batches():
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""

@@ -74,6 +74,15 @@ def main():
             json.dump(tj, open(tp, "w"), indent=1)
     if "SQ_LDS_BANK_CONFLICT" in avg:
         out["lds_bank_conflict_rate"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"])
+    if "TCC_EA0_RDREQ_sum" in avg:  # fabric read requests: one per 128-B line (MI355X_MICROARCH.md §HBM)
+        out["ea_rdreq_per_packet"] = avg["TCC_EA0_RDREQ_sum"] / n
+    tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+    if os.path.exists(tp):
+        tj = json.load(open(tp))
+        for k in ("lds_bank_conflict_rate", "ea_rdreq_per_packet"):
+            if k in out:
+                tj[k] = out[k]
+        json.dump(tj, open(tp, "w"), indent=1)
     if "GRBM_GUI_ACTIVE" in avg and out["kernels"]:
         k = next(iter(out["kernels"].values()))
         out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]

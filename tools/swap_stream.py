@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""configs[4] with live rule-table swaps mid-stream: classify throughput with commits between batches.
+
+Loads the adversarial table (IPv6 /128 deepest-prefix hits, last-slot ICMPv6 type/code rules,
+cross-family aliasing keys), then streams K resident batches through classify on one stream.
+Between batches it applies E key edits — each rewrites an existing key's value with another
+rule list (or deletes and re-adds it) — and commits them (an incremental epoch swap,
+DESIGN.md §4.1).  Reports Gpps with no edits, and with E edits committed after every batch
+(commit wall time included), plus the commit latency; the final per-rule totals are checked
+against the sum of the per-batch packet counts (stats persist across swaps).
+  python tools/swap_stream.py [--batch 16777216] [--batches 24] [--edits 1,100,1000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ingress-node-firewall_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--batches", type=int, default=24)
+    ap.add_argument("--edits", default="1,100,1000")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import infw
+    from infw import workloads as W
+    from infw.batch import SoaBatch
+
+    dev = torch.device("cuda", 0)
+    wl = W.Workload(W.CFG4_ADVERSARIAL)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)
+    wl.load_into(clf)
+    t0 = time.time()
+    clf.commit()
+    print(json.dumps({"cfg": 4, "entries": wl.n_entries, "initial_commit_s": round(time.time() - t0, 2)}), flush=True)
+    keys = wl.keys_bytes().reshape(-1, 24)
+    tmpl = np.ascontiguousarray(wl.templates_bytes().reshape(-1, 1200))
+    n = args.batch
+    batches = [SoaBatch.empty(n, dev) for _ in range(2)]
+    for j, b in enumerate(batches):
+        wl.gen_device(b, j * n, 0)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(7)
+
+    def run(edits):
+        clf.stats_reset()
+        commit_ms = []
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for k in range(args.batches):
+            clf.classify(batches[k & 1], results=res)
+            if edits:  # rewrite `edits` existing keys with other rule lists (one batch update), delete + re-add 1/16
+                idx = rng.integers(keys.shape[0], size=edits)  # O(edits); repeats are fine
+                for i in idx[: edits // 16]:
+                    clf.delete_rc(infw.LpmIpKeySt.from_buffer_copy(keys[i].tobytes()))  # -ENOENT on a repeat
+                sel = np.ascontiguousarray(keys[idx])
+                vi = rng.integers(tmpl.shape[0], size=edits).astype(np.uint32)
+                clf.update_batch_ptr(sel.ctypes.data, tmpl.ctypes.data, vi.ctypes.data, edits)
+                c0 = time.perf_counter()
+                clf.commit()  # epoch swap: the next batch reads the new epoch, this one finishes on the old
+                commit_ms.append((time.perf_counter() - c0) * 1e3)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - ts
+        st = clf.stats_read_all()
+        return wall, commit_ms, int(st[:, 0].sum() + st[:, 2].sum())
+
+    run(0)  # warm
+    run(1)  # warm the commit path (staging buffers, events)
+    base, _, counted0 = run(0)
+    out = {"batch": n, "batches": args.batches, "edits_per_commit": 0,
+           "gpps": round(n * args.batches / base / 1e9, 2), "counted": counted0}
+    print(json.dumps(out), flush=True)
+    for e in [int(x) for x in args.edits.split(",")]:
+        wall, cms, counted = run(e)
+        cms.sort()
+        print(json.dumps({"batch": n, "batches": args.batches, "edits_per_commit": e,
+                          "gpps": round(n * args.batches / wall / 1e9, 2),
+                          "commit_ms_median": round(cms[len(cms) // 2], 2), "commit_ms_max": round(cms[-1], 2),
+                          "commit_mode": clf.info()["commit_mode"], "full_reason": clf.info()["full_reason"],
+                          "counted": counted}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
