@@ -361,7 +361,7 @@ struct infw_table_info {
     uint64_t n_v6_groups;      /* (ifindex, /32) groups of IPv6 long prefixes */
     uint64_t n_v6_overflow;    /* groups with > 3 long prefixes (Waldvogel)   */
     uint32_t commit_mode;      /* INFW_COMMIT_*: how the last commit ran      */
-    uint32_t pad0;
+    uint32_t dt_parts;         /* value parts per (list, class) decision table */
     uint64_t patch_bytes;      /* bytes copied to the devices by it           */
     uint64_t dead_lists;       /* compiled lists no entry references (GC'd by */
                                /* the next full compile)                      */

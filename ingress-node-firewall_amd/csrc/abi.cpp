@@ -637,6 +637,7 @@ int infw_table_commit(infw_ctx *ctx) {
     in.n_v6_groups = h.n_buckets;
     in.n_v6_overflow = h.n_overflow_groups;
     in.commit_mode = mode;
+    in.dt_parts = 1u << h.dt_plog2;
     in.patch_bytes = patched;
     in.dead_lists = ctx->inc.dead_lists;
     memset(in.full_reason, 0, sizeof(in.full_reason));

@@ -328,11 +328,8 @@ void step_function(const std::vector<uint64_t> &recs, std::vector<uint32_t> &sta
     }
 }
 
-int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
-                      uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line *entry_out,
-                      std::vector<infw_dt_line> &leaves, uint32_t plog2) {
-    int rc = 0;
-    std::vector<uint64_t> per[INFW_NCLS];
+// Per-class first-match records of one 100-slot rule list (kernel.c:222-258 / :306-340).
+static void class_records(const uint8_t *val, std::vector<uint64_t> per[INFW_NCLS]) {
     for (int i = 0; i < INFW_MAX_RULES_PER_TARGET; i++) {
         const uint8_t *r = val + 12 * i;
         uint32_t rule_id = rd_le32(r);
@@ -368,6 +365,52 @@ int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
             break;
         }
     }
+}
+
+// Value parts per (list, class): the fewest (1, 2, 4, 8 or 16; as log2) for which at most
+// 1/256 of the (list, class, part) lines need a root + leaf, i.e. a second dependent table
+// line.  Fewer parts = fewer entry lines = more of them resident in L2: a rule set of short
+// lists (configs[1]: 10 rules) fits one line per (list, class) — 1/16 of the footprint —
+// while 99-rule lists (configs[2]) need 16 parts to stay at one line per packet.
+static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
+    uint64_t lines[5] = {}, over[5] = {};
+    std::vector<uint64_t> per[INFW_NCLS];
+    std::vector<uint32_t> starts, res;
+    for (const uint8_t *v : vals) {
+        for (auto &p : per) p.clear();
+        class_records(v, per);
+        for (int c = 0; c < INFW_NCLS; c++) {
+            step_function(per[c], starts, res);
+            bool compact = dt_compact_allowed();
+            for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
+            const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
+            for (uint32_t pl = 0; pl <= 4; pl++) {
+                const uint32_t span = 65536u >> pl;
+                uint32_t q = 0, nseg = 1;  // segments of part q: 1 + starts strictly inside it
+                for (size_t k = 1; k < starts.size(); k++) {
+                    while (starts[k] >= (q + 1) * span) {
+                        over[pl] += nseg > segs;
+                        nseg = 1;
+                        q++;
+                    }
+                    nseg += starts[k] > q * span;
+                }
+                for (; q < (1u << pl); q++, nseg = 1) over[pl] += nseg > segs;
+                lines[pl] += 1u << pl;
+            }
+        }
+    }
+    for (uint32_t pl = 0; pl < 4; pl++)
+        if (over[pl] * 256 <= lines[pl]) return pl;
+    return 4;
+}
+
+int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
+                      uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line *entry_out,
+                      std::vector<infw_dt_line> &leaves, uint32_t plog2) {
+    int rc = 0;
+    std::vector<uint64_t> per[INFW_NCLS];
+    class_records(val, per);
     for (int c = 0; c < INFW_DESC_STRIDE; c++) {
         if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], &entry_out[(size_t)c << plog2], leaves, plog2);
         if (c >= INFW_NCLS || per[c].empty()) {
@@ -471,9 +514,20 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     }
     out.n_lists = (uint32_t)list_of_vid.size();
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
-    // 16 parts per (list, class) while the entry lines fit 1 GiB (INFW_DT_PARTS=1|16 forces one form)
-    out.dt_plog2 = (uint64_t)out.n_lists * INFW_NCLS * 16 * sizeof(infw_dt_line) <= (1ull << 30) ? 4 : 0;
-    if (const char *e = getenv("INFW_DT_PARTS")) out.dt_plog2 = atoi(e) == 16 ? 4 : atoi(e) == 1 ? 0 : out.dt_plog2;
+    // value parts per (list, class): the fewest that keep one table line per packet (choose_dt_plog2),
+    // within a 1 GiB budget for the entry lines (INFW_DT_PARTS=1|2|4|8|16 forces one form)
+    {
+        std::vector<const uint8_t *> vals;
+        vals.reserve(list_of_vid.size());
+        for (const auto &p : list_of_vid) vals.push_back(m.pool.vals[p.first].data());
+        out.dt_plog2 = choose_dt_plog2(vals);
+        while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > (1ull << 30))
+            out.dt_plog2--;
+    }
+    if (const char *e = getenv("INFW_DT_PARTS")) {
+        const int v = atoi(e);
+        out.dt_plog2 = v == 16 ? 4 : v == 8 ? 3 : v == 4 ? 2 : v == 2 ? 1 : v == 1 ? 0 : out.dt_plog2;
+    }
     out.dte.assign(((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS) << out.dt_plog2, infw_dt_line{});
     out.dtl.clear();
     int dt_rc = 0;

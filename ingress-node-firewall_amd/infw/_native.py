@@ -106,7 +106,7 @@ class TableInfo(C.Structure):
                 ("n_long_levels", C.c_uint32), ("n_long_entries", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double),
                 ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64),
-                ("commit_mode", C.c_uint32), ("pad0", C.c_uint32), ("patch_bytes", C.c_uint64),
+                ("commit_mode", C.c_uint32), ("dt_parts", C.c_uint32), ("patch_bytes", C.c_uint64),
                 ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48)]
 
 

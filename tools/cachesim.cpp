@@ -79,7 +79,8 @@ struct Variant {
 int main(int argc, char **argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (4u << 20);
     infw_wl *wl = nullptr;
-    if (infw_wl_create(&wl, INFW_WL_CFG2_MIXED_1M, 0x1F000002ull, 0, 0)) return 1;
+    const int cfg = getenv("CACHESIM_CFG") ? atoi(getenv("CACHESIM_CFG")) : INFW_WL_CFG2_MIXED_1M;
+    if (infw_wl_create(&wl, cfg, 0x1F000000ull + cfg, 0, 0)) return 1;
     PendingMap m;
     m.max_entries = 1u << 22;
     const uint64_t ne = infw_wl_n_entries(wl);

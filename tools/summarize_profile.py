@@ -27,6 +27,10 @@ def main():
     tag = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 27
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    # only a configs[2] profile feeds profiles/traffic_cfg2.json (what bench.py reports beside its line)
+    bl = [l for l in open(os.path.join(src, "kt.stdout")) if l.startswith("{")] if os.path.exists(
+        os.path.join(src, "kt.stdout")) else []
+    is_cfg2 = not bl or json.loads(bl[-1])["config"]["workload"].startswith("cfg2")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in ("kt/kt_kernel_stats.csv", "kt/kt_domain_stats.csv"):
@@ -56,7 +60,7 @@ def main():
         out["hbm_bytes_per_launch"] = corr
         out["hbm_bytes_per_packet"] = corr / n
         out["hbm_bytes_per_packet_raw"] = raw / n
-        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
         tj = json.load(open(tp)) if os.path.exists(tp) else {}
         keep = {k: tj[k] for k in ("line_rates",) if k in tj}  # microbenchmark rates outlive a profile
         json.dump(dict({"tag": tag, "hbm_bytes_per_packet": corr / n, "hbm_bytes_per_packet_raw": raw / n,
@@ -66,7 +70,7 @@ def main():
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         out["l2_misses_per_packet"] = avg["TCC_MISS_sum"] / n
         out["l2_hits_per_packet"] = avg["TCC_HIT_sum"] / n
-        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
         if os.path.exists(tp):  # the random-line model bench.py reports beside the HBM roofline
             tj = json.load(open(tp))
             tj["l2_hits_per_packet"] = out["l2_hits_per_packet"]
@@ -76,7 +80,7 @@ def main():
         out["lds_bank_conflict_rate"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"])
     if "TCC_EA0_RDREQ_sum" in avg:  # fabric read requests: one per 128-B line (MI355X_MICROARCH.md §HBM)
         out["ea_rdreq_per_packet"] = avg["TCC_EA0_RDREQ_sum"] / n
-    tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+    tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
     if os.path.exists(tp):
         tj = json.load(open(tp))
         for k in ("lds_bank_conflict_rate", "ea_rdreq_per_packet"):
