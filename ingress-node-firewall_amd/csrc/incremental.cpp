@@ -54,6 +54,35 @@ void mark(std::vector<DirtyRange> &r, int buf, uint64_t off, uint64_t len) {
     if (len) r.push_back(DirtyRange{(uint32_t)buf, off, len});
 }
 
+// The entry of exactly /L (L <= 32 address bits) at address a on this ifindex, if any.
+inline const NodeVal *exact_short(const PendingMap &m, const uint8_t ifx_le[4], uint32_t a, uint32_t L) {
+    if (!m.len_count[L + 32]) return nullptr;
+    uint8_t md[20];
+    short_md(md, ifx_le, a);
+    NodeKey k;
+    k.plen = L + 32;
+    mask_bits(md, k.plen, k.md, 20);
+    auto it = m.nodes.find(k);
+    return it == m.nodes.end() ? nullptr : &it->second;
+}
+
+// Longest-match answers over the /L block at address a, for every /Lend sub-block: depth-first
+// over the block's sub-prefixes, one probe per populated length and node, starting from v = the
+// answer of the lengths below L.  About two probes per sub-block, where probing every length for
+// every sub-block costs (Lend - L + 1) — a /16 edit re-derives its 256 tbl24 words with ~511
+// probes instead of ~256 x 9.
+template <class Leaf>
+void descend(const PendingMap &m, const uint8_t ifx_le[4], uint32_t a, uint32_t L, uint32_t Lend,
+             const NodeVal *v, Leaf &leaf) {
+    if (const NodeVal *e = exact_short(m, ifx_le, a, L)) v = e;
+    if (L == Lend) {
+        leaf(a, v);
+        return;
+    }
+    descend(m, ifx_le, a, L + 1, Lend, v, leaf);
+    descend(m, ifx_le, a | (1u << (31 - L)), L + 1, Lend, v, leaf);
+}
+
 }  // namespace
 
 int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
@@ -217,33 +246,37 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (e.P <= 32) shorts.push_back(&e);
     std::sort(shorts.begin(), shorts.end(), [](const Edit *a, const Edit *b) { return a->P < b->P; });
     uint8_t md[20];
-    auto refill_group = [&](const uint8_t *ifx, uint32_t i24, uint32_t g, uint32_t j0, uint32_t cnt) {
+    // tbl8 entries [j0, j0 + 2^(32 - P)) of group g under /24 i24: the /P block's answers at /32,
+    // from base = the answer of the lengths below P
+    auto refill_group = [&](const uint8_t *ifx, uint32_t i24, uint32_t g, uint32_t j0, uint32_t P, const NodeVal *base) {
         uint32_t *t8 = &h.tbl8[(size_t)g << 8];
-        for (uint32_t j = j0; j < j0 + cnt; j++) {
-            short_md(md, ifx, i24 << 8 | j);
-            t8[j] = list1(m.longest(md, 32, 64));
-        }
-        mark(ranges, TB_TBL8, (((uint64_t)g << 8) + j0) * 4, (uint64_t)cnt * 4);
+        auto leaf = [&](uint32_t a, const NodeVal *v) { t8[a & 0xFFu] = list1(v); };
+        descend(m, ifx, i24 << 8 | j0, P, 32, base, leaf);
+        mark(ranges, TB_TBL8, (((uint64_t)g << 8) + j0) * 4, (4ull << (32 - P)));
     };
     for (const Edit *e : shorts) {
         const uint8_t *ifx = e->key->md;
         uint64_t *t24 = &h.tbl24[(size_t)e->slot << 24];
         const uint64_t gkey = (uint64_t)e->slot << 24;
+        const uint32_t a = e->P ? e->a32 & (~0u << (32 - e->P)) : 0u;
+        short_md(md, ifx, a);
+        const NodeVal *below = e->P ? m.longest(md, 32, 32 + e->P - 1) : nullptr;  // lengths < P
         if (e->P <= 24) {
-            const uint32_t i0 = e->a32 >> 8, cnt = 1u << (24 - e->P);
-            for (uint32_t i = i0; i < i0 + cnt; i++) {
+            const uint32_t i0 = a >> 8, cnt = 1u << (24 - e->P);
+            auto leaf24 = [&](uint32_t a24, const NodeVal *v) {  // v: the longest entry <= /24 of this word
+                const uint32_t i = a24 >> 8;
                 auto g = h.tbl8_of.find(gkey | i);
                 if (g != h.tbl8_of.end()) {
-                    refill_group(ifx, i, g->second, 0, 256);
+                    refill_group(ifx, i, g->second, 0, 24, v);
                     t24[i] = infw_d24_encode(&h.tbl8[(size_t)g->second << 8], g->second, h.d24_inline);
                 } else {
-                    short_md(md, ifx, i << 8);
-                    t24[i] = list1(m.longest(md, 32, 56));
+                    t24[i] = list1(v);
                 }
-            }
+            };
+            descend(m, ifx, a, e->P, 24, below, leaf24);
             mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i0) * 8, (uint64_t)cnt * 8);
         } else {
-            const uint32_t i = e->a32 >> 8;
+            const uint32_t i = a >> 8;
             auto it = h.tbl8_of.find(gkey | i);
             uint32_t g;
             if (it != h.tbl8_of.end()) {
@@ -257,7 +290,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                 h.tbl8_of[gkey | i] = g;
                 h.n_tbl8_groups++;
             }
-            refill_group(ifx, i, g, e->a32 & 0xFFu, 1u << (32 - e->P));
+            refill_group(ifx, i, g, a & 0xFFu, e->P, below);
             t24[i] = infw_d24_encode(&h.tbl8[(size_t)g << 8], g, h.d24_inline);
             mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 8, 8);
         }

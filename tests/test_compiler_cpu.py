@@ -203,3 +203,35 @@ def test_host_sanitizer_walk():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(["make", "-s", "asan"], cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_many_ifindexes_host_walk():
+    """400 ifindexes (ifindex map outside the kernel's LDS copy, compressed short table chosen by size):
+    the compiled image walked on the CPU equals the oracle (the GPU form is test_gpu_parity.test_many_ifindexes)."""
+    import struct
+    import orc
+    from frames import snapshots  # noqa: F401
+    from test_incremental_cpu import _packets_for
+    rng = random.Random(400)
+    ifs = rng.sample(range(1, 1 << 20), 400)
+    ents = {}
+    for i in range(6000):
+        ifx = ifs[i % 400]
+        if rng.random() < 0.6:
+            L = rng.choice([0, 8, 16, 20, 24, 25, 28, 32])
+            ip = rng.getrandbits(32).to_bytes(4, "big") + bytes(12)
+        else:
+            L = rng.choice([16, 32, 40, 48, 56, 64, 96, 128])
+            ip = rng.getrandbits(128).to_bytes(16, "big")
+        ents[struct.pack("<II", L + 32, ifx) + ip] = _val(rng, i)
+    c = infw.Classifier(devices=[], max_entries=len(ents) + 16, flags=infw.F_HOST_ONLY)
+    m = orc.OracleMap(max_entries=len(ents) + 16)
+    for k, v in ents.items():
+        assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    c.commit()
+    hdr, cap, pl, ifx = _packets_for(rng.sample(list(ents), 2000), rng, 2)
+    ifx[::7] = np.array([rng.randrange(1 << 20, 1 << 21) for _ in range(ifx[::7].size)], np.uint32)
+    want, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=4)
+    got = c.debug_walk(W.pack_frames(hdr, cap, pl, ifx))
+    assert np.array_equal(got, want)
+    assert c.info()["n_if_slots"] == 400

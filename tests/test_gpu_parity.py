@@ -440,6 +440,45 @@ def test_commits_while_batches_in_flight():
     assert not np.array_equal(want_a, m3.classify_frames(*wl.frames(0, n), nthreads=8)[0])  # the edits matter
 
 
+@pytest.mark.parametrize("n_if", [100, 129, 400])
+def test_many_ifindexes(n_if):
+    """The ifindex map outside LDS (> 128 ifindexes: the map no longer fits the kernel's 256-entry LDS copy) and
+    the short-table form chosen by size (> 32 ifindexes: DIR-24-8 would exceed 4 GiB -> compressed 16-8-8):
+    random v4/v6 prefixes on n_if ifindexes, packets aimed at them and at unknown ifindexes, vs the oracle."""
+    import random
+    import struct
+    import orc
+    from test_compiler_cpu import _val
+    from test_incremental_cpu import _packets_for
+    rng = random.Random(n_if)
+    ifs = rng.sample(range(1, 1 << 20), n_if)
+    ents = {}
+    for i in range(6000):
+        ifx = ifs[i % n_if]
+        if rng.random() < 0.6:
+            L = rng.choice([0, 8, 16, 20, 24, 25, 28, 32])
+            ip = rng.getrandbits(32).to_bytes(4, "big") + bytes(12)
+        else:
+            L = rng.choice([16, 32, 40, 48, 56, 64, 96, 128])
+            ip = rng.getrandbits(128).to_bytes(16, "big")
+        ents[struct.pack("<II", L + 32, ifx) + ip] = _val(rng, i)
+    clf = infw.Classifier(devices=[0], max_entries=len(ents) + 16)
+    m = orc.OracleMap(max_entries=len(ents) + 16)
+    for k, v in ents.items():
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    clf.commit()
+    keys = list(ents)
+    hdr, cap, pl, ifx = _packets_for(rng.sample(keys, 3000), rng, 3)
+    ifx[::7] = np.array([rng.randrange(1 << 20, 1 << 21) for _ in range(ifx[::7].size)], np.uint32)  # unknown
+    want, _, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    dev = torch.device("cuda", 0)
+    clf.stats_reset()
+    got, _ = gpu_run(clf, SoaBatch.from_tuples(W.pack_frames(hdr, cap, pl, ifx), dev), len(ifx))
+    assert np.array_equal(got, want)
+    assert np.array_equal(clf.stats_read_all(), wst)
+    assert (want != 0).mean() > 0.3
+
+
 def test_classify_host_batches():
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
