@@ -25,7 +25,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "ingress-node-firewall_amd")]
 
-ALGO_BYTES_PER_PKT = 36  # 32 B SoA tuple in + 4 B result word out
+ALGO_BYTES_PER_PKT = 36  # standard layout: 32 B SoA tuple in + 4 B result word out
+# family-compact layout (infw_batch_soa_c): 4 address bytes per packet + 12 more per IPv6 packet, + 16 B of
+# ifindex/pkt_len/meta/l4word in, + 4 B result word out = 24 + 12 * (IPv6 share) bytes per packet
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md)
 METRIC = "Mpps classified @1M prefixes x 100 rules, 1/2/4/8 GPUs; % HBM BW roofline"
 
@@ -43,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_cfg2.json"))
+    ap.add_argument("--layout", default="compact", choices=["compact", "standard"],
+                    help="batch address layout (include/infw.h): family-compact (default) or 16-B standard")
     return ap.parse_args()
 
 
@@ -85,6 +89,12 @@ def main():
     n = args.batch
     batch = SoaBatch.empty(n, dev)
     wl.gen_device(batch, start=rank * n, dev_ordinal=local)
+    if args.layout == "compact":  # the packer's production layout (infw_pack_frames_c); converted untimed here
+        batch_c = clf.compact(batch, dev=0)
+        n6 = int(((batch.meta & 0xFFFF) == 0x86DD).sum().item())
+        algo_bytes = 24 + 12 * n6 / n
+    else:
+        algo_bytes = ALGO_BYTES_PER_PKT
     results = torch.empty(n, dtype=torch.int32, device=dev)
     stats = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # this step's per-rule counters
     total = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # job totals (all ranks)
@@ -96,7 +106,10 @@ def main():
         stats.zero_()
         if ev is not None:
             ev[0].record(stream)
-        clf.classify(batch, results=results, stream=stream)
+        if args.layout == "compact":
+            clf.classify_c(batch_c, results=results, stream=stream)
+        else:
+            clf.classify(batch, results=results, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -126,7 +139,7 @@ def main():
     total_pkts = n * world * args.steps
     mpps = total_pkts / elapsed / 1e6
     avg_kern_ms = sum(kern_ms) / len(kern_ms)
-    achieved = ALGO_BYTES_PER_PKT * n / (avg_kern_ms * 1e-3) / 1e9
+    achieved = algo_bytes * n / (avg_kern_ms * 1e-3) / 1e9
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
 
     traffic = None
@@ -192,9 +205,10 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "traffic_from": traffic_from,
-            "kernel": "classify_kernel<512, 0>",
+            "kernel": "classify_kernel<512, 0>" + (" (family-compact layout)" if args.layout == "compact" else ""),
             "kernel_ms_avg": round(avg_kern_ms, 4),
-            "algorithmic_bytes_per_packet": ALGO_BYTES_PER_PKT,
+            "algorithmic_bytes_per_packet": round(algo_bytes, 3),
+            "layout": args.layout,
             "random_line_model": line_model,
             **extra,
         },

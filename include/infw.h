@@ -146,6 +146,36 @@ struct infw_batch_soa_out {
     uint32_t *l4word;
 };
 
+/* Family-compact layout of the same bytes (infw_classify_c): the 12 address   */
+/* bytes only IPv6 packets have are stored only for them.                     */
+/*   saddr4   4 B per packet: frame[26..29] (IPv4) or frame[22..25] (IPv6)     */
+/*   v6tail   per group g of INFW_V6_GROUP packets, a 12*INFW_V6_GROUP-byte   */
+/*            block at g * 12 * INFW_V6_GROUP: frame[26..37] of the group's    */
+/*            packets whose meta ethertype is 0x86DD, in packet order, packed */
+/*            from the start of the block (4-byte aligned)                     */
+/*   ifindex, pkt_len, meta, l4word as in infw_batch_soa                       */
+/* A reader touches only the first 12 * (IPv6 packets of the group) bytes of  */
+/* a block: 4 + 12 * (IPv6 share) address bytes per packet instead of 16.      */
+#define INFW_V6_GROUP 64
+struct infw_batch_soa_c {
+    const uint32_t *saddr4;
+    const uint8_t *v6tail;
+    const uint32_t *ifindex;
+    const uint32_t *pkt_len;
+    const uint32_t *meta;
+    const uint32_t *l4word;
+};
+
+/* Writable family-compact destination of infw_pack_frames_c.                */
+struct infw_batch_soa_c_out {
+    uint32_t *saddr4;
+    uint8_t *v6tail;
+    uint32_t *ifindex;
+    uint32_t *pkt_len;
+    uint32_t *meta;
+    uint32_t *l4word;
+};
+
 typedef struct infw_ctx infw_ctx;
 
 /* ------------------------------------------------------------------------ */
@@ -223,6 +253,13 @@ int infw_table_commit(infw_ctx *ctx);
 /* ------------------------------------------------------------------------ */
 int infw_classify(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
                   uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+/* infw_classify over the family-compact layout (identical results).          */
+int infw_classify_c(infw_ctx *ctx, int dev, const struct infw_batch_soa_c *in, uint64_t n,
+                    uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+/* Standard -> family-compact address layout on the device: saddr4 (n words) */
+/* and v6tail (ceil(n / INFW_V6_GROUP) blocks); the other streams are shared.  */
+int infw_soa_compact(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
+                     uint32_t *saddr4, uint8_t *v6tail, void *stream);
 
 /* Launch shape of the classify kernel (tuning; defaults 512 / 0 / 4, or the  */
 /* INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU environment variables):    */
@@ -235,6 +272,11 @@ int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu)
 /* above, run as a kernel over frames already in HBM).  Asynchronous.          */
 int infw_pack_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
                      const struct infw_batch_soa_out *out, void *stream);
+/* infw_pack_frames into the family-compact layout (the production feed of     */
+/* infw_classify_c): v6tail blocks of groups with fewer IPv6 packets are only  */
+/* written up to their last tail.                                             */
+int infw_pack_frames_c(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
+                       const struct infw_batch_soa_c_out *out, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */

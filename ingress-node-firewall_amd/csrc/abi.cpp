@@ -21,7 +21,10 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
                                     infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
-                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots);
+                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots,
+                                    const infw_batch_soa_c *in_c);
+extern "C" int infw_launch_soa_compact(const infw_batch_soa *in, uint64_t n, uint32_t *saddr4, uint8_t *v6tail,
+                                       uint32_t cus, hipStream_t stream);
 
 extern "C" int infw_launch_scatter(const uint32_t *staging, const void *descs, uint32_t n, uint32_t cus,
                                    hipStream_t stream);
@@ -31,7 +34,7 @@ struct infw_patch_desc {  // patch.hip
 };
 
 extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
-                                       uint32_t cus, hipStream_t stream);
+                                       const infw_batch_soa_c_out *out_c, uint32_t cus, hipStream_t stream);
 
 namespace infw {
 
@@ -686,24 +689,63 @@ int infw_classify(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n,
     return infw_classify_ex(ctx, dev, in, n, result_words, xdp_verdicts, nullptr, stream);
 }
 
+static int classify_impl(infw_ctx *ctx, int dev, const infw_batch_soa *in, const infw_batch_soa_c *in_c, uint64_t n,
+                         uint32_t *result_words, uint8_t *xdp_verdicts, const struct infw_classify_ex *ex, void *stream);
+
 int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n, uint32_t *result_words,
                      uint8_t *xdp_verdicts, const struct infw_classify_ex *ex, void *stream) {
+    return classify_impl(ctx, dev, in, nullptr, n, result_words, xdp_verdicts, ex, stream);
+}
+
+int infw_classify_c(infw_ctx *ctx, int dev, const infw_batch_soa_c *in, uint64_t n, uint32_t *result_words,
+                    uint8_t *xdp_verdicts, void *stream) {
+    if (!in) return -EINVAL;
+    if (n && (!in->saddr4 || !in->v6tail || ((uintptr_t)in->v6tail & 3) != 0)) {
+        set_error("classify_c: null or misaligned address stream");
+        return -EINVAL;
+    }
+    return classify_impl(ctx, dev, nullptr, in, n, result_words, xdp_verdicts, nullptr, stream);
+}
+
+int infw_soa_compact(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n, uint32_t *saddr4, uint8_t *v6tail,
+                     void *stream) {
+    if (!ctx || !in || (n && (!in->saddr || !in->meta || !saddr4 || !v6tail))) return -EINVAL;
+    if (ctx->devs.empty()) return -ENODEV;
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (((uintptr_t)in->saddr & 15) != 0 || ((uintptr_t)v6tail & 3) != 0) {
+        set_error("soa_compact: saddr must be 16-byte and v6tail 4-byte aligned");
+        return -EINVAL;
+    }
+    Device &d = ctx->devs[dev];
+    DeviceGuard g(d.ordinal);
+    if (!g.ok) return -ENODEV;
+    if (infw_launch_soa_compact(in, n, saddr4, v6tail, d.cus, static_cast<hipStream_t>(stream))) {
+        set_error(std::string("soa_compact launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    return 0;
+}
+
+static int classify_impl(infw_ctx *ctx, int dev, const infw_batch_soa *in, const infw_batch_soa_c *in_c, uint64_t n,
+                         uint32_t *result_words, uint8_t *xdp_verdicts, const struct infw_classify_ex *ex, void *stream) {
     if (ex && (ex->size < sizeof(struct infw_classify_ex) || ex->flags != 0 || (ex->events_cap && !ex->events) ||
                (ex->events && !ex->events_count))) {
         set_error("classify_ex: bad options");
         return -EINVAL;
     }
-    if (!ctx || !in) return -EINVAL;
+    if (!ctx || (!in && !in_c)) return -EINVAL;
     if (ctx->devs.empty()) {
         set_error("classify: host-only context has no device tables");
         return -ENODEV;
     }
     if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
-    if (n && (!in->saddr || !in->ifindex || !in->pkt_len || !in->meta || !in->l4word)) {
+    const uint32_t *ifx = in ? in->ifindex : in_c->ifindex, *pl = in ? in->pkt_len : in_c->pkt_len;
+    const uint32_t *mt = in ? in->meta : in_c->meta, *l4 = in ? in->l4word : in_c->l4word;
+    if (n && ((in && !in->saddr) || !ifx || !pl || !mt || !l4)) {
         set_error("classify: null input stream");
         return -EINVAL;
     }
-    if (((uintptr_t)in->saddr & 15) != 0) {
+    if (in && ((uintptr_t)in->saddr & 15) != 0) {
         set_error("classify: saddr must be 16-byte aligned");
         return -EINVAL;
     }
@@ -726,7 +768,7 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t 
     int rc = infw_launch_classify(&ep->view, in, n, result_words, xdp_verdicts, d.stats, d.cus, ctx->block,
                                   ctx->group, ctx->blocks_per_cu, static_cast<hipStream_t>(stream),
                                   evs ? ex->events : nullptr, evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr,
-                                  ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots);
+                                  ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots, in_c);
     if (rc) {
         set_error(std::string("classify launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
@@ -812,7 +854,7 @@ int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_
         const infw_batch_soa db{s.saddr, s.ifindex, s.pkt_len, s.meta, s.l4word};
         if (infw_launch_classify(&ep->view, &db, c, results ? s.res : nullptr, verdicts ? s.ver : nullptr, d.stats,
                                  d.cus, ctx->block, ctx->group, ctx->blocks_per_cu, pipe->run, nullptr, 0, nullptr,
-                                 ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots)) {
+                                 ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots, nullptr)) {
             set_error(std::string("classify_host launch failed: ") + hipGetErrorString(hipGetLastError()));
             return -EIO;
         }
@@ -910,7 +952,30 @@ int infw_pack_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_
     }
     DeviceGuard g(ctx->devs[dev].ordinal);
     if (!g.ok) return -ENODEV;
-    if (infw_launch_pack_frames(fb, n, out, ctx->devs[dev].cus, static_cast<hipStream_t>(stream))) {
+    if (infw_launch_pack_frames(fb, n, out, nullptr, ctx->devs[dev].cus, static_cast<hipStream_t>(stream))) {
+        set_error(std::string("pack launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    return 0;
+}
+
+int infw_pack_frames_c(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_c_out *out,
+                       void *stream) {
+    if (!ctx || !fb || !out) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("pack_frames_c: host-only context");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (n && (!fb->frames || !fb->linear_len || !fb->ifindex || (!fb->offsets && !fb->stride) || !out->saddr4 ||
+              !out->v6tail || !out->ifindex || !out->pkt_len || !out->meta || !out->l4word ||
+              ((uintptr_t)out->v6tail & 3))) {
+        set_error("pack_frames_c: bad arguments");
+        return -EINVAL;
+    }
+    DeviceGuard g(ctx->devs[dev].ordinal);
+    if (!g.ok) return -ENODEV;
+    if (infw_launch_pack_frames(fb, n, nullptr, out, ctx->devs[dev].cus, static_cast<hipStream_t>(stream))) {
         set_error(std::string("pack launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }

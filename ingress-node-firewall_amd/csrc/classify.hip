@@ -184,6 +184,16 @@ __device__ __forceinline__ uint32_t v6_long_dev(const infw_dev_tables &T, uint32
     }
 }
 
+// The batch as the kernel reads it: the 16-B address layout (infw_batch_soa) or the
+// family-compact one (infw_batch_soa_c: 4 address bytes per packet + the IPv6 packets'
+// remaining 12 bytes packed at the front of a 768-B block per 64-packet group).
+struct BatchIn {
+    const uint8_t *saddr;    // 16 B per packet (standard layout)
+    const uint32_t *saddr4;  // compact layout
+    const uint8_t *v6tail;
+    const uint32_t *ifindex, *pkt_len, *meta, *l4word;
+};
+
 // G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
 struct EventSink {
     infw_event_rec *rec;
@@ -247,8 +257,8 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kPrefetch = !(kAblate & 128)>
-__global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const infw_batch_soa in,
+          bool kDebug = false, bool kC = false, bool kPrefetch = !(kAblate & 128)>
+__global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
@@ -288,14 +298,18 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 l4w = __builtin_nontemporal_load(&in.l4word[i]);
                 ifx = __builtin_nontemporal_load(&in.ifindex[i]);
                 plen = __builtin_nontemporal_load(&in.pkt_len[i]);
-                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(sa4) + i);
-                sa = make_uint4(t[0], t[1], t[2], t[3]);
+                if (kC) {
+                    sa = make_uint4(__builtin_nontemporal_load(&in.saddr4[i]), 0u, 0u, 0u);
+                } else {
+                    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(sa4) + i);
+                    sa = make_uint4(t[0], t[1], t[2], t[3]);
+                }
             } else {
                 meta = in.meta[i];
                 l4w = in.l4word[i];
                 ifx = in.ifindex[i];
                 plen = in.pkt_len[i];
-                sa = sa4[i];
+                sa = kC ? make_uint4(in.saddr4[i], 0u, 0u, 0u) : sa4[i];
             }
         }
     };
@@ -308,7 +322,19 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         const bool valid = i < n;
         if (!kPrefetch && base != (uint64_t)blockIdx.x * kBlock) load_tuple(i, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         const uint32_t meta = valid ? n_meta : 0, l4w = n_l4w, ifx = n_ifx, plen = n_plen;
-        const uint4 sa = n_sa;
+        uint4 sa = n_sa;
+        if (kC) {  // IPv6 packets: address bytes 4..15 from the group's packed block (rank among its IPv6 lanes)
+            const bool is6 = (meta & 0xFFFFu) == 0x86DDu;
+            const uint64_t m6 = __ballot(is6);
+            if (is6) {
+                const uint32_t rank = __popcll(m6 & ((1ull << lane) - 1));
+                const uint32_t *t = reinterpret_cast<const uint32_t *>(in.v6tail + (i >> 6) * (INFW_V6_GROUP * 12ull)) +
+                                    3 * rank;
+                sa.y = __builtin_nontemporal_load(t);
+                sa.z = __builtin_nontemporal_load(t + 1);
+                sa.w = __builtin_nontemporal_load(t + 2);
+            }
+        }
         if (kPrefetch) load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         int cls = 0;
         uint32_t val = 0;
@@ -503,15 +529,15 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false>
-void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
+          bool kDebug = false, bool kC = false>
+void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug>), dim3(g), dim3(kBlock), 0, stream,
-                       *T, *in, n, results, verdicts, st, sb);
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC>), dim3(g), dim3(kBlock), 0,
+                       stream, *T, *in, n, results, verdicts, st, sb);
 }
 
 }  // namespace
@@ -519,25 +545,43 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
 // Host-side launcher (called from abi.cpp).
 //   block: 256 or 512 threads; group: 0 = decision tables (default), else the
 //   one-lane-per-rule ballot scan with that many packets in flight (1, 4, 8);
-//   blocks_per_cu: resident workgroups per CU (LDS: 24 KiB each).
-extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
+//   blocks_per_cu: resident workgroups per CU (LDS: 34 KiB each).
+//   in_c (optional): the family-compact layout instead of `in` (default launch shape).
+extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in_s, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
                                     infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
-                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots) {
+                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots,
+                                    const infw_batch_soa_c *in_c) {
     if (n == 0) return 0;
+    BatchIn bi{};
+    if (in_c) {
+        bi = BatchIn{nullptr, in_c->saddr4, in_c->v6tail, in_c->ifindex, in_c->pkt_len, in_c->meta, in_c->l4word};
+    } else {
+        bi = BatchIn{in_s->saddr, nullptr, nullptr, in_s->ifindex, in_s->pkt_len, in_s->meta, in_s->l4word};
+    }
+    const BatchIn *in = &bi;
+    const uint32_t bpc = (uint32_t)blocks_per_cu;
     if (ev_count || dbg_fp) {  // sidebands: the default launch shape with them compiled in
         auto *stt = reinterpret_cast<unsigned long long *>(stats);
         const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
                           DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
-        const uint32_t bpc = (uint32_t)blocks_per_cu;
-        if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-        else if (ev_count) launch<512, 0, 0, true, 8, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-        else launch<512, 0, 0, false, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+        if (in_c) {
+            if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else if (ev_count) launch<512, 0, 0, true, 8, false, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else launch<512, 0, 0, false, 8, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+        } else {
+            if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else if (ev_count) launch<512, 0, 0, true, 8, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else launch<512, 0, 0, false, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+        }
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
-    const uint32_t bpc = (uint32_t)blocks_per_cu;
+    if (in_c) {  // the compact layout runs the default shape (tuning variants use the standard layout)
+        launch<512, 0, 0, false, 8, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     if (const char *e = getenv("INFW_ABLATE")) {  // diagnostic builds of the 512/8 shape; results are not valid
         switch (atoi(e)) {
         case 0: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;

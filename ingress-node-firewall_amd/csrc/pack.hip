@@ -18,14 +18,28 @@ __device__ __forceinline__ uint32_t byte_at(const uint8_t *f, uint32_t cap, uint
     return off < cap ? (uint32_t)f[off] : 0u;
 }
 
-__global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch fb, uint64_t n,
-                                                          infw_batch_soa_out out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint8_t *f = fb.frames + (fb.offsets ? fb.offsets[i] : i * fb.stride);
-        const uint32_t cap = fb.linear_len[i];
-        const uint32_t plen = fb.pkt_len ? fb.pkt_len[i] : cap;
-        uint32_t ethertype = 0, proto = 0, l4off = 0, soff = 0, slen = 0;
-        if (cap >= 14) {
+struct PackOut {  // standard (saddr) or family-compact (saddr4 + v6tail) address layout
+    uint8_t *saddr;
+    uint32_t *saddr4;
+    uint8_t *v6tail;
+    uint32_t *ifindex, *pkt_len, *meta, *l4word;
+};
+
+template <bool kC>
+__global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch fb, uint64_t n, PackOut out) {
+    // wave-uniform trip count: the compact layout ranks a group's IPv6 lanes with one ballot
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t ethertype = 0, proto = 0, l4off = 0, soff = 0, slen = 0, cap = 0, plen = 0;
+        const uint8_t *f = nullptr;
+        if (valid) {
+            f = fb.frames + (fb.offsets ? fb.offsets[i] : i * fb.stride);
+            cap = fb.linear_len[i];
+            plen = fb.pkt_len ? fb.pkt_len[i] : cap;
+        }
+        if (valid && cap >= 14) {
             ethertype = byte_at(f, cap, 12) << 8 | byte_at(f, cap, 13);
             if (ethertype == 0x0800) {
                 proto = byte_at(f, cap, 23);
@@ -41,21 +55,80 @@ __global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch
         uint32_t l4 = 0;
         if (l4off)
             for (uint32_t k = 0; k < 4; k++) l4 |= byte_at(f, cap, l4off + k) << (8 * k);
-        reinterpret_cast<uint4 *>(out.saddr)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-        out.ifindex[i] = fb.ifindex[i];
-        out.pkt_len[i] = plen;
-        out.meta[i] = ethertype | proto << 16 | (cap > 255u ? 255u : cap) << 24;
-        out.l4word[i] = l4;
+        if (kC) {
+            const bool is6 = ethertype == 0x86DD;  // == the meta ethertype the classifier ranks by
+            const uint64_t m6 = __ballot(is6);
+            if (valid) out.saddr4[i] = sw[0];
+            if (is6) {
+                const uint32_t rank = __popcll(m6 & ((1ull << (threadIdx.x & 63u)) - 1));
+                uint32_t *t = reinterpret_cast<uint32_t *>(out.v6tail + (i >> 6) * (12ull * INFW_V6_GROUP)) + 3 * rank;
+                t[0] = sw[1];
+                t[1] = sw[2];
+                t[2] = sw[3];
+            }
+        } else if (valid) {
+            reinterpret_cast<uint4 *>(out.saddr)[i] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+        }
+        if (valid) {
+            out.ifindex[i] = fb.ifindex[i];
+            out.pkt_len[i] = plen;
+            out.meta[i] = ethertype | proto << 16 | (cap > 255u ? 255u : cap) << 24;
+            out.l4word[i] = l4;
+        }
     }
 }
 
 }  // namespace
 
+// out: standard layout, or (out == nullptr) out_c: the family-compact layout.
 extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
-                                       uint32_t cus, hipStream_t stream) {
+                                       const infw_batch_soa_c_out *out_c, uint32_t cus, hipStream_t stream) {
     if (n == 0) return 0;
     uint64_t blocks = (n + 255) / 256, cap = (uint64_t)cus * 8;
-    hipLaunchKernelGGL(pack_frames_kernel, dim3((uint32_t)(blocks < cap ? blocks : cap)), dim3(256), 0, stream, *fb,
-                       n, *out);
+    const dim3 grid((uint32_t)(blocks < cap ? blocks : cap));
+    if (out) {
+        const PackOut o{out->saddr, nullptr, nullptr, out->ifindex, out->pkt_len, out->meta, out->l4word};
+        hipLaunchKernelGGL(pack_frames_kernel<false>, grid, dim3(256), 0, stream, *fb, n, o);
+    } else {
+        const PackOut o{nullptr, out_c->saddr4, out_c->v6tail, out_c->ifindex, out_c->pkt_len, out_c->meta, out_c->l4word};
+        hipLaunchKernelGGL(pack_frames_kernel<true>, grid, dim3(256), 0, stream, *fb, n, o);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Standard -> family-compact address layout (infw_batch_soa_c): one lane per packet,
+// packets of a wave = one INFW_V6_GROUP group; an IPv6 lane's rank among the group's
+// IPv6 lanes places its 12 tail bytes.
+namespace {
+__global__ __launch_bounds__(256) void soa_compact_kernel(const uint8_t *__restrict__ saddr, const uint32_t *__restrict__ meta,
+                                                          uint64_t n, uint32_t *__restrict__ saddr4,
+                                                          uint8_t *__restrict__ v6tail) {
+    static_assert(INFW_V6_GROUP == 64, "one wave per group");
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(saddr + 16 * (valid ? i : 0));
+        const bool is6 = valid && (meta[i] & 0xFFFFu) == 0x86DDu;
+        const uint64_t m6 = __ballot(is6);
+        if (valid) saddr4[i] = s[0];
+        if (is6) {
+            const uint32_t lane = threadIdx.x & 63u;
+            const uint32_t rank = __popcll(m6 & ((1ull << lane) - 1));
+            uint32_t *t = reinterpret_cast<uint32_t *>(v6tail + (i >> 6) * (12ull * INFW_V6_GROUP)) + 3 * rank;
+            t[0] = s[1];
+            t[1] = s[2];
+            t[2] = s[3];
+        }
+    }
+}
+}  // namespace
+
+extern "C" int infw_launch_soa_compact(const infw_batch_soa *in, uint64_t n, uint32_t *saddr4, uint8_t *v6tail,
+                                       uint32_t cus, hipStream_t stream) {
+    if (n == 0) return 0;
+    const uint64_t blocks = (n + 255) / 256, cap = 8ull * cus;
+    hipLaunchKernelGGL(soa_compact_kernel, dim3((uint32_t)(blocks < cap ? blocks : cap)), dim3(256), 0, stream,
+                       in->saddr, in->meta, n, saddr4, v6tail);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -75,6 +75,15 @@ class BatchSoa(C.Structure):
                 ("meta", C.c_void_p), ("l4word", C.c_void_p)]
 
 
+class BatchSoaC(C.Structure):
+    """struct infw_batch_soa_c (include/infw.h): the family-compact address layout."""
+    _fields_ = [("saddr4", C.c_void_p), ("v6tail", C.c_void_p), ("ifindex", C.c_void_p), ("pkt_len", C.c_void_p),
+                ("meta", C.c_void_p), ("l4word", C.c_void_p)]
+
+
+V6_GROUP = 64  # INFW_V6_GROUP
+
+
 class FrameBatch(C.Structure):
     """struct infw_frame_batch (include/infw.h)."""
     _fields_ = [("frames", C.c_void_p), ("offsets", C.c_void_p), ("stride", C.c_uint64), ("linear_len", C.c_void_p),
@@ -123,7 +132,7 @@ ABI_SYMBOLS = [
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
-    "infw_host_register", "infw_host_unregister",
+    "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c",
 ]
 
 
@@ -164,6 +173,11 @@ _sig = {
     "infw_pack_frames": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoa), C.c_void_p]),
     "infw_classify_host": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
                                      C.c_uint64]),
+    "infw_classify_c": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoaC), C.c_uint64, C.c_void_p, C.c_void_p,
+                                  C.c_void_p]),
+    "infw_pack_frames_c": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoaC), C.c_void_p]),
+    "infw_soa_compact": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
+                                   C.c_void_p]),
     "infw_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "infw_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "infw_stats_read": (C.c_int, [C.c_void_p, C.c_uint32, P(RuleStatisticsSt), P(C.c_int)]),

@@ -54,3 +54,39 @@ class SoaBatch:
 
     def slice(self, a: int, b: int) -> "SoaBatch":
         return SoaBatch(self.saddr[a:b], self.ifindex[a:b], self.pkt_len[a:b], self.meta[a:b], self.l4word[a:b])
+
+
+@dataclass
+class SoaBatchC:
+    """Family-compact layout (include/infw.h: infw_batch_soa_c): 4 address bytes per packet plus, per group
+    of 64 packets, the IPv6 packets' remaining 12 bytes packed at the front of a 768-B block.  The other
+    streams are the standard batch's tensors (shared, not copied)."""
+    saddr4: "torch.Tensor"   # int32 [n]
+    v6tail: "torch.Tensor"   # uint8 [ceil(n / 64) * 768]
+    ifindex: "torch.Tensor"
+    pkt_len: "torch.Tensor"
+    meta: "torch.Tensor"
+    l4word: "torch.Tensor"
+
+    @property
+    def n(self) -> int:
+        return int(self.ifindex.shape[0])
+
+    @property
+    def device(self):
+        return self.ifindex.device
+
+    @staticmethod
+    def empty(n: int, device) -> "SoaBatchC":
+        import torch
+        i32 = lambda: torch.empty(n, dtype=torch.int32, device=device)
+        return SoaBatchC(i32(), torch.zeros(((n + 63) // 64) * 768, dtype=torch.uint8, device=device), i32(), i32(),
+                         i32(), i32())
+
+    @staticmethod
+    def empty_for(b: SoaBatch) -> "SoaBatchC":
+        import torch
+        groups = (b.n + 63) // 64
+        return SoaBatchC(torch.empty(b.n, dtype=torch.int32, device=b.device),
+                         torch.zeros(groups * 768, dtype=torch.uint8, device=b.device),
+                         b.ifindex, b.pkt_len, b.meta, b.l4word)

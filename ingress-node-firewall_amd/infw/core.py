@@ -157,6 +157,32 @@ class Classifier:
                            results.data_ptr() if results is not None else 0,
                            verdicts.data_ptr() if verdicts is not None else 0, sp)
 
+    def compact(self, batch, dev: int = 0, stream=None):
+        """infw_soa_compact: a SoaBatchC of `batch` (address bytes re-laid out on the device, other streams shared)."""
+        from .batch import SoaBatchC
+        out = SoaBatchC.empty_for(batch)
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(batch.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        b = N.BatchSoa(batch.saddr.data_ptr(), batch.ifindex.data_ptr(), batch.pkt_len.data_ptr(),
+                       batch.meta.data_ptr(), batch.l4word.data_ptr())
+        check(N.lib.infw_soa_compact(self._ctx, dev, C.byref(b), batch.n, out.saddr4.data_ptr(), out.v6tail.data_ptr(),
+                                     sp), "soa_compact")
+        return out
+
+    def classify_c(self, batch_c, results=None, verdicts=None, dev: int = 0, stream=None) -> None:
+        """infw_classify_c over a SoaBatchC (identical results to classify on the standard layout)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(batch_c.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        b = N.BatchSoaC(batch_c.saddr4.data_ptr(), batch_c.v6tail.data_ptr(), batch_c.ifindex.data_ptr(),
+                        batch_c.pkt_len.data_ptr(), batch_c.meta.data_ptr(), batch_c.l4word.data_ptr())
+        check(N.lib.infw_classify_c(self._ctx, dev, C.byref(b), batch_c.n,
+                                    results.data_ptr() if results is not None else None,
+                                    verdicts.data_ptr() if verdicts is not None else None, sp), "classify_c")
+
     def classify_events(self, batch, events, events_count, results=None, verdicts=None, dev: int = 0,
                         stream=None) -> None:
         """classify + the deny-event stream (kernel.c:392-399) into `events` (uint8 tensor of cap*24 B)
@@ -204,6 +230,20 @@ class Classifier:
         o = N.BatchSoa(out.saddr.data_ptr(), out.ifindex.data_ptr(), out.pkt_len.data_ptr(), out.meta.data_ptr(),
                        out.l4word.data_ptr())
         check(N.lib.infw_pack_frames(self._ctx, dev, C.byref(fb), out.n, C.byref(o), sp), "pack_frames")
+
+    def pack_frames_c(self, frames, linear_len, ifindex, out_c, pkt_len=None, offsets=None, stride: int = 0,
+                      dev: int = 0, stream=None) -> None:
+        """Frames in device memory -> the family-compact batch `out_c` (infw.batch.SoaBatchC) on the device."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        fb = N.FrameBatch(frames.data_ptr(), offsets.data_ptr() if offsets is not None else None, stride,
+                          linear_len.data_ptr(), pkt_len.data_ptr() if pkt_len is not None else None,
+                          ifindex.data_ptr())
+        o = N.BatchSoaC(out_c.saddr4.data_ptr(), out_c.v6tail.data_ptr(), out_c.ifindex.data_ptr(),
+                        out_c.pkt_len.data_ptr(), out_c.meta.data_ptr(), out_c.l4word.data_ptr())
+        check(N.lib.infw_pack_frames_c(self._ctx, dev, C.byref(fb), out_c.n, C.byref(o), sp), "pack_frames_c")
 
     def set_launch(self, block: int = 512, scan_group: int = 0, blocks_per_cu: int = 4) -> None:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""

@@ -50,8 +50,10 @@ def stats_from_results(results: np.ndarray, pkt_len: np.ndarray) -> np.ndarray:
     return out
 
 
-def check_cfg(cfg: int, n: int, n_prefixes: int = 0, n_templates: int = 0, start: int = 0, device=None):
-    """End-to-end parity on one config: device-generated SoA vs host frames + oracle."""
+def check_cfg(cfg: int, n: int, n_prefixes: int = 0, n_templates: int = 0, start: int = 0, device=None,
+              layout: str = "standard"):
+    """End-to-end parity on one config: device-generated SoA vs host frames + oracle.
+    layout "compact": the batch is re-laid out by infw_soa_compact and classified by infw_classify_c."""
     import torch
     from infw.batch import SoaBatch
     device = device or torch.device("cuda", 0)
@@ -68,7 +70,15 @@ def check_cfg(cfg: int, n: int, n_prefixes: int = 0, n_templates: int = 0, start
     dev_tuples = batch.to_tuples()
     assert np.array_equal(dev_tuples, host_tuples), "device generator != host frames packed"
     clf.stats_reset()
-    gres, gver = gpu_run(clf, batch, n)
+    if layout == "compact":
+        bc = clf.compact(batch)
+        res = torch.empty(n, dtype=torch.int32, device=device)
+        ver = torch.empty(n, dtype=torch.uint8, device=device)
+        clf.classify_c(bc, results=res, verdicts=ver)
+        torch.cuda.synchronize(device)
+        gres, gver = res.cpu().numpy().view(np.uint32), ver.cpu().numpy()
+    else:
+        gres, gver = gpu_run(clf, batch, n)
     gstats = clf.stats_read_all()
     return dict(wl=wl, clf=clf, oracle=m, ores=ores, over=over, ostats=ostats, gres=gres, gver=gver,
                 gstats=gstats, pkt_len=pl, batch=batch)

@@ -252,6 +252,23 @@ def test_pack_frames_on_device():
     torch.cuda.synchronize()
     h2, c2, p2 = snapshots(fr)
     assert np.array_equal(out2.to_tuples(), W.pack_frames(h2, c2, p2, ifs))
+    # the family-compact output: the same bytes as infw_soa_compact of the standard output, and the oracle's results
+    from infw.batch import SoaBatchC
+    for std, (fbuf, flen, fifx, fkw) in ((out, (torch.from_numpy(hdr).to(dev), t(np.minimum(cap, 80)), t(ifx),
+                                                 dict(pkt_len=t(pl), stride=80))),
+                                         (out2, (buf, t(lens), t(ifs),
+                                                 dict(offsets=torch.from_numpy(offs.view(np.int64)).to(dev))))):
+        oc = SoaBatchC.empty(std.n, dev)
+        clf.pack_frames_c(fbuf, flen, fifx, oc, **fkw)
+        ref = clf.compact(std)
+        torch.cuda.synchronize()
+        assert torch.equal(oc.saddr4, ref.saddr4) and torch.equal(oc.v6tail, ref.v6tail)
+        for a, b in ((oc.ifindex, std.ifindex), (oc.pkt_len, std.pkt_len), (oc.meta, std.meta), (oc.l4word, std.l4word)):
+            assert torch.equal(a, b)
+        res = torch.empty(std.n, dtype=torch.int32, device=dev)
+        clf.classify_c(oc, results=res)
+        g_std, _ = gpu_run(clf, std, std.n)
+        assert np.array_equal(res.cpu().numpy().view(np.uint32), g_std)
 
 
 @pytest.mark.parametrize("short_table", ["dir24", "compressed"])
@@ -477,6 +494,33 @@ def test_many_ifindexes(n_if):
     assert np.array_equal(got, want)
     assert np.array_equal(clf.stats_read_all(), wst)
     assert (want != 0).mean() > 0.3
+
+
+@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG2_MIXED_1M, 50000, 256), (W.CFG4_ADVERSARIAL, 20000, 64),
+                                            (W.CFG1_V4_10K, 0, 0)])
+def test_compact_layout(cfg, npfx, ntmpl):
+    """infw_soa_compact + infw_classify_c: the family-compact address layout gives the oracle's result words,
+    verdicts and counters (ragged batch: the last 64-packet group is partial; cfg1 has no IPv6 packets)."""
+    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = (1 << 18) + 37
+    b = SoaBatch.empty(n, dev)
+    wl.gen_device(b, 7, 0)
+    bc = clf.compact(b)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    ver = torch.empty(n, dtype=torch.uint8, device=dev)
+    clf.stats_reset()
+    clf.classify_c(bc, results=res, verdicts=ver)
+    torch.cuda.synchronize()
+    hdr, cap, pl, ifx = wl.frames(7, n)
+    want, wver, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    assert np.array_equal(res.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(ver.cpu().numpy(), wver)
+    assert np.array_equal(clf.stats_read_all(), wst)
 
 
 def test_classify_host_batches():
