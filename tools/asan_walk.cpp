@@ -7,6 +7,7 @@
 #include <stdlib.h>
 
 #include <string>
+#include <vector>
 
 #include "../ingress-node-firewall_amd/csrc/infw_internal.h"
 
@@ -83,6 +84,103 @@ static int run_case(int n_keys, int v4_share, int max_rules, int mode, int seed)
     return 0;
 }
 
+// Incremental commits under ASan: random churn (value rewrites, deletes, re-adds, new keys on known
+// ifindexes) patched into the compiled image by patch_tables; after every patch the image must walk
+// exactly like a fresh compile of the same map.
+static uint32_t walk_result(const infw_dev_tables &t, int pk, uint32_t ifx, const uint32_t sa[4], int cls, uint32_t v) {
+    const uint32_t l1 = infw_lpm(t, pk, ifx, sa);
+    return l1 ? infw_dt_eval(t, l1 - 1, cls, v) : 0u;
+}
+
+static int run_churn(int n_keys, int seed) {
+    rs = 0xC2B2AE3D27D4EB4Full * (uint64_t)(seed + 7);
+    PendingMap m;
+    m.max_entries = 1u << 20;
+    static uint8_t val[1200];
+    std::vector<lpm_ip_key_st> keys;
+    auto rand_key = [&]() {
+        lpm_ip_key_st k;
+        memset(&k, 0, sizeof k);
+        k.ingress_ifindex = 1 + rnd() % 3;
+        const bool v4 = rnd() % 2;
+        const uint32_t len = v4 ? 8 + rnd() % 25 : 33 + rnd() % 96;
+        k.prefixLen = len + 32;
+        for (int b = 0; b < 16; b++) k.ip_data[b] = (uint8_t)rnd();
+        if (rnd() % 3 == 0) k.ip_data[0] = k.ip_data[1] = k.ip_data[2] = 10;
+        return k;
+    };
+    for (int i = 0; i < n_keys; i++) {
+        lpm_ip_key_st k = rand_key();
+        random_value(val, 1 + rnd() % 40);
+        if (m.update(&k, val, 0) == 0) keys.push_back(k);
+    }
+    HostTables h;
+    IncState inc;
+    if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
+    m.dirty.clear();
+    int patched = 0, full = 0;
+    for (int round = 0; round < 12; round++) {
+        const int edits = 1 + rnd() % (round % 3 == 0 ? 400 : 40);
+        for (int e = 0; e < edits; e++) {
+            const uint32_t r = rnd() % 10;
+            if (r < 5 && !keys.empty()) {  // rewrite
+                random_value(val, 1 + rnd() % 40);
+                m.update(&keys[rnd() % keys.size()], val, 0);
+            } else if (r < 7 && !keys.empty()) {
+                m.remove(&keys[rnd() % keys.size()]);
+            } else {
+                lpm_ip_key_st k = rand_key();
+                random_value(val, 1 + rnd() % 40);
+                if (m.update(&k, val, 0) == 0) keys.push_back(k);
+            }
+        }
+        std::vector<DirtyRange> ranges;
+        std::string why;
+        int rc = patch_tables(m, h, inc, ranges, &why);
+        if (rc != 0) {  // a layout change: recompile, as infw_table_commit does
+            full++;
+            h = HostTables();
+            inc = IncState();
+            if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
+        } else {
+            patched++;
+            for (const DirtyRange &d : ranges) {
+                const void *p;
+                size_t bytes;
+                host_buffer(h, (int)d.buf, &p, &bytes);
+                if (d.off + d.len > bytes + 64) {
+                    fprintf(stderr, "churn: range past buffer %u: %llu + %llu > %zu\n", d.buf,
+                            (unsigned long long)d.off, (unsigned long long)d.len, bytes);
+                    return -1;
+                }
+            }
+        }
+        m.dirty.clear();
+        HostTables f;
+        if (compile_tables(m, f, INFW_SHORT_DIR24, 4ull << 30)) return -1;
+        const infw_dev_tables tp = h.view(), tf = f.view();
+        for (int i = 0; i < 40000; i++) {
+            uint32_t sa[4] = {rnd(), rnd(), rnd(), rnd()};
+            if (rnd() % 2 && !keys.empty()) {  // aim at a key's prefix
+                const lpm_ip_key_st &k = keys[rnd() % keys.size()];
+                memcpy(sa, k.ip_data, 4);
+            }
+            if (rnd() % 3 == 0) sa[0] = (sa[0] & 0xFF000000u) | 0x000A0A0Au;
+            const int pk = rnd() % 2 ? INFW_PK_V4 : INFW_PK_V6;
+            const uint32_t ifx = 1 + rnd() % 3;
+            const int cls = (int)(rnd() % INFW_NCLS);
+            const uint32_t v = rnd() & 0xFFFF;
+            const uint32_t a = walk_result(tp, pk, ifx, sa, cls, v), b = walk_result(tf, pk, ifx, sa, cls, v);
+            if (a != b) {
+                fprintf(stderr, "churn seed %d round %d: patched %x vs fresh %x\n", seed, round, a, b);
+                return -1;
+            }
+        }
+    }
+    printf("churn keys %d seed %d: %d patched commits, %d full\n", n_keys, seed, patched, full);
+    return 0;
+}
+
 // DIR-24-8 word encoding: every 256-value /24 pattern decodes to itself, inline or via its group.
 static int check_d24_words() {
     static uint32_t tbl8[256];
@@ -109,6 +207,7 @@ static int check_d24_words() {
 
 int main() {
     int bad = check_d24_words();
+    for (int s = 0; s < 3; s++) bad |= run_churn(3000, s) != 0;
     const int modes[3] = {INFW_SHORT_DIR24, INFW_SHORT_COMPRESSED, -1};
     for (int s = 0; s < 3; s++)
         for (int mi = 0; mi < 3; mi++) {
