@@ -71,6 +71,7 @@ struct Variant {
     int slot_bytes = 64;  // bytes per (list, class, part) slot: a compact leaf of 20 / 10 / 5 segments
     int entry_stride = 64;
     int dense_short = 0;  // 1: short-table lookups touch one 8-B word per matched prefix, prefixes sorted by (slot, address)
+    int cuckoo = 0;   // 1: IPv6 groups in the two-choice table above (absent groups touch both buckets)
     int pairing = 0;  // 1: compiled parts, entry line at ((list * 16 + part) * 8 + cls) * 64 (classes of one part adjacent)
 };
 
@@ -125,8 +126,8 @@ int main(int argc, char **argv) {
                             {"quarters16", false, false, 16}, {"parts16x32B", false, false, 16, 32},
                             {"parts32x32B", false, false, 32, 32}, {"parts32x16B", false, false, 32, 16},
                             {"parts64x16B", false, false, 64, 16}, {"parts8x32B", false, false, 8, 32},
-                            {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 1},
-                            {"dense_short", false, false, 0, 64, 64, 1}};
+                            {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 0, 1},
+                            {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1}};
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -271,6 +272,38 @@ int main(int argc, char **argv) {
                lines, (double)el / n, (double)eh / el, (double)bl / n, (double)bh / bl);
         fflush(stdout);
     }
+    // IPv6 group census (records per (slot, /32) group) and a what-if: the groups in a two-choice
+    // table of 64-B buckets holding CUCKOO_SLOTS single-record groups each, at CUCKOO_LOAD
+    std::unordered_map<uint64_t, uint64_t> cuckoo_at;  // group key -> bucket index (+ 1 << 62 if secondary)
+    uint64_t cuckoo_buckets = 1;
+    {
+        uint64_t hist[6] = {}, ng = 0;
+        std::vector<uint64_t> gk;
+        for (const auto &b : h.btab)
+            if (b.tag) {
+                hist[b.n == INFW_BUCKET_OVERFLOW ? 5 : b.n < 4 ? b.n : 4]++;
+                ng++;
+                gk.push_back((uint64_t)(b.tag - 1) << 32 | b.top);
+            }
+        const double load = getenv("CUCKOO_LOAD") ? atof(getenv("CUCKOO_LOAD")) : 0.5;
+        const uint32_t slots = getenv("CUCKOO_SLOTS") ? atoi(getenv("CUCKOO_SLOTS")) : 2;
+        while ((double)cuckoo_buckets * slots * load < (double)ng) cuckoo_buckets <<= 1;
+        std::vector<uint32_t> fill(cuckoo_buckets, 0);
+        uint64_t sec = 0, fail = 0;
+        for (uint64_t k : gk) {
+            const uint64_t h1 = infw_bucket_hash((uint32_t)(k >> 32), (uint32_t)k) & (cuckoo_buckets - 1);
+            const uint64_t h2 = (infw_bucket_hash((uint32_t)(k >> 32) ^ 0x5bd1e995u, (uint32_t)k) >> 7) & (cuckoo_buckets - 1);
+            if (fill[h1] < slots) { fill[h1]++; cuckoo_at[k] = h1; }
+            else if (fill[h2] < slots) { fill[h2]++; cuckoo_at[k] = h2 | 1ull << 62; sec++; }
+            else fail++;
+        }
+        printf("{\"v6_groups\": %llu, \"records_hist\": [%llu, %llu, %llu, %llu, %llu, %llu], \"cuckoo\": {\"load\": %.2f, "
+               "\"slots\": %u, \"buckets\": %llu, \"secondary\": %.4f, \"unplaced\": %llu}}\n",
+               (unsigned long long)ng, (unsigned long long)hist[0], (unsigned long long)hist[1],
+               (unsigned long long)hist[2], (unsigned long long)hist[3], (unsigned long long)hist[4],
+               (unsigned long long)hist[5], load, slots, (unsigned long long)cuckoo_buckets, (double)sec / ng,
+               (unsigned long long)fail);
+    }
     if (getenv("CACHESIM_LDS_ONLY")) return 0;
     const char *only = getenv("CACHESIM_VARIANTS");
     for (const Variant &V : vars) {
@@ -293,6 +326,14 @@ int main(int argc, char **argv) {
                 if (pk == INFW_PK_V6 && t.n_levels) {
                     const uint64_t bi = infw_bucket_hash((uint32_t)slot, a32) & t.bmask;  // first probe only
                     tc[nt++] = {S_BUCKET, 0 * kSpace + bi * 64};
+                    if (V.cuckoo) {
+                        const uint64_t gk = (uint64_t)slot << 32 | a32;
+                        auto it = cuckoo_at.find(gk);
+                        const uint64_t h1 = infw_bucket_hash((uint32_t)slot, a32) & (cuckoo_buckets - 1);
+                        const uint64_t h2 = (infw_bucket_hash((uint32_t)slot ^ 0x5bd1e995u, a32) >> 7) & (cuckoo_buckets - 1);
+                        tc[nt - 1].addr = 5 * kSpace + h1 * 64;
+                        if (it == cuckoo_at.end() || (it->second >> 62)) tc[nt++] = {S_BUCKET, 5 * kSpace + h2 * 64};
+                    }
                     lng = infw_v6_long(t, (uint32_t)slot, a32, q);
                 }
                 if (!lng) {
