@@ -45,8 +45,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_cfg2.json"))
-    ap.add_argument("--layout", default="compact", choices=["compact", "standard"],
-                    help="batch address layout (include/infw.h): family-compact (default) or 16-B standard")
+    ap.add_argument("--layout", default="standard", choices=["compact", "standard"],
+                    help="batch address layout (include/infw.h): 16-B standard (default) or family-compact")
     return ap.parse_args()
 
 

@@ -261,10 +261,11 @@ int infw_classify_c(infw_ctx *ctx, int dev, const struct infw_batch_soa_c *in, u
 int infw_soa_compact(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
                      uint32_t *saddr4, uint8_t *v6tail, void *stream);
 
-/* Launch shape of the classify kernel (tuning; defaults 512 / 0 / 4, or the  */
-/* INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU environment variables):    */
-/* block 256|512 threads; scan_group 0 = first-match decision tables, or    */
-/* 1|4|8 = one-lane-per-rule ballot scan with that many packets in flight; */
+/* Launch shape of the classify kernel (tuning; defaults 768 / 0 / 2 = 24    */
+/* waves per CU, or the INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU       */
+/* environment variables): block 256|512|768 threads (other multiples of 64  */
+/* run as 512 x 3); scan_group 0 = first-match decision tables, or 1|4|8 =   */
+/* one-lane-per-rule ballot scan with that many packets in flight;           */
 /* blocks_per_cu resident workgroups per CU.                                  */
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
 

@@ -222,7 +222,7 @@ struct infw_ctx {
     IncState inc;
     std::mutex epoch_mu;  // guards devs[*].epoch swaps vs classify snapshots
     // launch shape of the classify kernel (infw_set_launch / INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU)
-    int block = 512, group = 0, blocks_per_cu = 4;
+    int block = 768, group = 0, blocks_per_cu = 2;
     uint32_t debug_lookup = 0;  // kernel.c:78
     uint64_t epoch_no = 0;
     uint64_t committed_gen = ~0ull;
@@ -415,12 +415,16 @@ int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_
         *out = ctx.release();
         return 0;
     }
-    if (const char *e = getenv("INFW_BLOCK")) ctx->block = atoi(e) == 256 ? 256 : 512;
+    // default shape: 2 x 768-thread workgroups per CU = 24 waves (6 per SIMD). Measured on MI355X at configs[2]:
+    // 24 waves beat 32 (512 x 4) by 8 % and 16 (512 x 2) by 17 % — fewer lines in flight thrash the L2 less —
+    // and 768 lets the LDS word cache hold 4096 entries (tools/tune.py, profiles/r01i/occupancy_sweep.log)
+    ctx->block = 768;
+    if (const char *e = getenv("INFW_BLOCK")) ctx->block = atoi(e) == 256 ? 256 : atoi(e) == 512 ? 512 : 768;
     if (const char *e = getenv("INFW_SCAN_GROUP")) {
         int g = atoi(e);
         ctx->group = (g == 1 || g == 4 || g == 8) ? g : 0;
     }
-    ctx->blocks_per_cu = ctx->block == 512 ? 4 : 6;  // 24 KiB LDS per workgroup: 32 / 24 waves per CU
+    ctx->blocks_per_cu = ctx->block == 768 ? 2 : ctx->block == 512 ? 3 : 6;  // 24 waves per CU
     if (const char *e = getenv("INFW_BLOCKS_PER_CU")) ctx->blocks_per_cu = atoi(e) > 0 ? atoi(e) : ctx->blocks_per_cu;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -983,7 +987,7 @@ int infw_pack_frames_c(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint6
 }
 
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu) {
-    if (!ctx || (block != 256 && block != 512) || (scan_group != 0 && scan_group != 1 && scan_group != 4 && scan_group != 8) ||
+    if (!ctx || block < 64 || block > 1024 || block % 64 || (scan_group != 0 && scan_group != 1 && scan_group != 4 && scan_group != 8) ||
         blocks_per_cu < 1 || blocks_per_cu > 32)
         return -EINVAL;
     ctx->block = block;

@@ -29,7 +29,7 @@ namespace {
 constexpr int kStatKeys = INFW_MAX_TARGETS;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kIfLds = 256;  // ifindex map entries mirrored in LDS
-constexpr uint32_t kC24 = 1024;   // per-workgroup LDS cache of plain DIR-24-8 words
+constexpr int kC24LogDefault = 10;  // per-workgroup LDS cache of plain DIR-24-8 words: 1 << kC24Log entries
 
 // Short-table lookup through the workgroup's LDS cache of DIR-24-8 words.  Traffic
 // is heavy-tailed (at configs[2] the top 500 of 1M prefixes carry ~65 % of the hits),
@@ -45,12 +45,12 @@ __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t
     return T.tbl8[((uint64_t)(uint32_t)w << 8) | (a32 & 0xFFu)];
 }
 
-template <bool kCache>
+template <bool kCache, int kLog>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                         unsigned long long *s_c24) {
     if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u) return infw_short_lookup(T, slot, a32);
     const uint32_t key = slot << 24 | a32 >> 8;
-    const uint32_t idx = (key * 0x9E3779B1u) >> 22;  // 10 bits
+    const uint32_t idx = (key * 0x9E3779B1u) >> (32 - kLog);
     const unsigned long long e = s_c24[idx];
     if ((e >> 63) && (uint32_t)(e >> 31) == key) return (uint32_t)e & 0x7FFFFFFFu;
     const uint64_t w = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
@@ -257,7 +257,7 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, bool kPrefetch = !(kAblate & 128)>
+          bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, bool kPrefetch = !(kAblate & 128)>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -268,7 +268,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     __shared__ unsigned long long s_by[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
     // diagnostic 32: no LDS word cache; the 256-thread shapes (6 blocks per CU) have no LDS room for it
-    constexpr bool kCache = !(kAblate & 32) && kBlock == 512;
+    constexpr bool kCache = !(kAblate & 32) && kBlock >= 384;
+    constexpr uint32_t kC24 = 1u << kC24Log;
     __shared__ unsigned long long s_c24[kCache ? kC24 : 1];
     if (kCache)
         for (int i = threadIdx.x; i < (int)kC24; i += kBlock) s_c24[i] = 0;
@@ -291,10 +292,11 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
     // the next tile's tuple is loaded while the current tile walks the tables:
     // the stream's latency overlaps the first table lookups instead of adding to them
-    auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa) {
+    auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa,
+                          bool with_meta = true) {
         if (i < n) {
             if (!(kAblate & 16)) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL (16: plain, diagnostic)
-                meta = __builtin_nontemporal_load(&in.meta[i]);
+                if (with_meta) meta = __builtin_nontemporal_load(&in.meta[i]);
                 l4w = __builtin_nontemporal_load(&in.l4word[i]);
                 ifx = __builtin_nontemporal_load(&in.ifindex[i]);
                 plen = __builtin_nontemporal_load(&in.pkt_len[i]);
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     sa = make_uint4(t[0], t[1], t[2], t[3]);
                 }
             } else {
-                meta = in.meta[i];
+                if (with_meta) meta = in.meta[i];
                 l4w = in.l4word[i];
                 ifx = in.ifindex[i];
                 plen = in.pkt_len[i];
@@ -313,9 +315,33 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             }
         }
     };
+    // compact layout: an IPv6 packet's address bytes 4..15 sit in its 64-packet group's block at its rank
+    // among the group's IPv6 lanes (one ballot of the meta ethertype)
+    auto load_tail = [&](uint64_t i, uint32_t meta, uint32_t &t0, uint32_t &t1, uint32_t &t2) {
+        const bool is6 = i < n && (meta & 0xFFFFu) == 0x86DDu;
+        const uint64_t m6 = __ballot(is6);
+        if (is6) {
+            const uint32_t rank = __popcll(m6 & ((1ull << lane) - 1));
+            const uint32_t *t = reinterpret_cast<const uint32_t *>(in.v6tail + (i >> 6) * (INFW_V6_GROUP * 12ull)) + 3 * rank;
+            t0 = __builtin_nontemporal_load(t);
+            t1 = __builtin_nontemporal_load(t + 1);
+            t2 = __builtin_nontemporal_load(t + 2);
+        }
+    };
     uint32_t n_meta = 0, n_l4w = 0, n_ifx = 0, n_plen = 0;
     uint4 n_sa = make_uint4(0, 0, 0, 0);
-    load_tuple((uint64_t)blockIdx.x * kBlock + threadIdx.x, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+    // compact + prefetch: the meta word runs two tiles ahead, so the next tile's tail loads can be issued a
+    // whole tile early like the rest of its tuple (issued with the tile's own table loads, the tails' HBM
+    // latency would hold back the in-order return of the bucket probes)
+    uint32_t n_meta2 = 0, n_t0 = 0, n_t1 = 0, n_t2 = 0;
+    {
+        const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        load_tuple(i0, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+        if (kC && kPrefetch) {
+            if (i0 + stride < n) n_meta2 = __builtin_nontemporal_load(&in.meta[i0 + stride]);
+            load_tail(i0, n_meta, n_t0, n_t1, n_t2);
+        }
+    }
 
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
         const uint64_t i = base + threadIdx.x;
@@ -323,19 +349,24 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         if (!kPrefetch && base != (uint64_t)blockIdx.x * kBlock) load_tuple(i, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         const uint32_t meta = valid ? n_meta : 0, l4w = n_l4w, ifx = n_ifx, plen = n_plen;
         uint4 sa = n_sa;
-        if (kC) {  // IPv6 packets: address bytes 4..15 from the group's packed block (rank among its IPv6 lanes)
-            const bool is6 = (meta & 0xFFFFu) == 0x86DDu;
-            const uint64_t m6 = __ballot(is6);
-            if (is6) {
-                const uint32_t rank = __popcll(m6 & ((1ull << lane) - 1));
-                const uint32_t *t = reinterpret_cast<const uint32_t *>(in.v6tail + (i >> 6) * (INFW_V6_GROUP * 12ull)) +
-                                    3 * rank;
-                sa.y = __builtin_nontemporal_load(t);
-                sa.z = __builtin_nontemporal_load(t + 1);
-                sa.w = __builtin_nontemporal_load(t + 2);
+        if (kC && kPrefetch) {
+            sa.y = n_t0;
+            sa.z = n_t1;
+            sa.w = n_t2;
+        } else if (kC) {  // no prefetch (diagnostic 128): the tails load with the tile
+            load_tail(i, meta, sa.y, sa.z, sa.w);
+        }
+        if (kPrefetch) {
+            if (kC) {
+                const uint32_t m1 = n_meta2;  // tile t+1's meta, loaded one tile ago
+                load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa, false);
+                if (i + 2 * stride < n) n_meta2 = __builtin_nontemporal_load(&in.meta[i + 2 * stride]);
+                load_tail(i + stride, m1, n_t0, n_t1, n_t2);
+                n_meta = m1;
+            } else {
+                load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
             }
         }
-        if (kPrefetch) load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         int cls = 0;
         uint32_t val = 0;
         const int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
@@ -381,7 +412,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     const bool v6 = pk == INFW_PK_V6 && T.n_levels;
                     const bool d24 = T.short_mode == INFW_SHORT_DIR24;
                     const uint32_t key = (uint32_t)slot << 24 | a32 >> 8;
-                    const uint32_t cidx = (key * 0x9E3779B1u) >> 22;
+                    const uint32_t cidx = (key * 0x9E3779B1u) >> (32 - kC24Log);
                     bool need24 = !v6 && d24;
                     uint32_t sh = 0;
                     if (kCache && need24 && slot < 256) {
@@ -409,13 +440,13 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     } else if (!v6 && !d24) {
                         sh = infw_short_lookup(T, (uint32_t)slot, a32);  // compressed / no short table
                     }
-                    if (v6 && !lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
+                    if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 } else if (slot >= 0) {  // diagnostic 512: the sequential form (bucket round, then tbl24 round)
                     const uint32_t a32 = infw_bswap32(sa.x);
                     uint32_t lng = 0, sh = 0;
                     if (pk == INFW_PK_V6 && T.n_levels) lng = v6_long_dev(T, (uint32_t)slot, a32, sw);
-                    if (!lng) sh = short_lookup_cached<kCache>(T, (uint32_t)slot, a32, s_c24);
+                    if (!lng) sh = short_lookup_cached<kCache, kC24Log>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 }
             }
@@ -529,15 +560,34 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false>
+          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC>), dim3(g), dim3(kBlock), 0,
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog>), dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
+}
+
+// The decision-table kernel without sidebands: launch shape (block, resident blocks per CU) and
+// LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.
+template <bool kC>
+bool launch_shape(int block, uint32_t bpc, int log, uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
+                  uint64_t n, uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
+    if (block == 512 && bpc == 4 && log == 10) launch<512, 0, 0, false, 8, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 512 && bpc == 3 && log == 10) launch<512, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 896 && bpc == 2 && log == 12) launch<896, 0, 0, false, 7, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 640 && bpc == 3 && log == 11) launch<640, 0, 0, false, 8, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 448 && bpc == 4 && log == 10) launch<448, 0, 0, false, 7, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 384 && bpc == 4 && log == 10) launch<384, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else return false;
+    return true;
 }
 
 }  // namespace
@@ -561,26 +611,39 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         bi = BatchIn{in_s->saddr, nullptr, nullptr, in_s->ifindex, in_s->pkt_len, in_s->meta, in_s->l4word};
     }
     const BatchIn *in = &bi;
-    const uint32_t bpc = (uint32_t)blocks_per_cu;
-    if (ev_count || dbg_fp) {  // sidebands: the default launch shape with them compiled in
+    uint32_t bpc = (uint32_t)blocks_per_cu;
+    if (ev_count || dbg_fp) {  // sidebands: 512 x 3 (24 waves per CU) with them compiled in
+        bpc = 3;
         auto *stt = reinterpret_cast<unsigned long long *>(stats);
         const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
                           DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
         if (in_c) {
-            if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else if (ev_count) launch<512, 0, 0, true, 8, false, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else launch<512, 0, 0, false, 8, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            if (ev_count && dbg_fp) launch<512, 0, 0, true, 6, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else if (ev_count) launch<512, 0, 0, true, 6, false, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else launch<512, 0, 0, false, 6, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
         } else {
-            if (ev_count && dbg_fp) launch<512, 0, 0, true, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else if (ev_count) launch<512, 0, 0, true, 8, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else launch<512, 0, 0, false, 8, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            if (ev_count && dbg_fp) launch<512, 0, 0, true, 6, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else if (ev_count) launch<512, 0, 0, true, 6, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
+            else launch<512, 0, 0, false, 6, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
         }
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
-    if (in_c) {  // the compact layout runs the default shape (tuning variants use the standard layout)
-        launch<512, 0, 0, false, 8, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    const char *env_l = getenv("INFW_C24LOG");  // tuning
+    const int env_log = env_l ? atoi(env_l) : 0;
+    const int log = env_log ? env_log : (block == 768 ? 12 : bpc <= 3 ? 11 : 10);
+    if (group == 0 && !getenv("INFW_ABLATE")) {
+        const bool ok = in_c ? launch_shape<true>(block, bpc, log, cus, T, in, n, results, verdicts, st, stream)
+                             : launch_shape<false>(block, bpc, log, cus, T, in, n, results, verdicts, st, stream);
+        if (ok) return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (in_c) {  // any other shape: the compact layout runs 512 x 3
+        launch<512, 0, 0, false, 6, false, true, 11>(3, cus, T, in, n, results, verdicts, st, stream);
         return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (block != 256 && block != 512) {  // shapes without their own instantiation: 512 x 3
+        block = 512;
+        bpc = 3;
     }
     if (const char *e = getenv("INFW_ABLATE")) {  // diagnostic builds of the 512/8 shape; results are not valid
         switch (atoi(e)) {

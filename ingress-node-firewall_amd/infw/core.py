@@ -245,7 +245,7 @@ class Classifier:
                         out_c.pkt_len.data_ptr(), out_c.meta.data_ptr(), out_c.l4word.data_ptr())
         check(N.lib.infw_pack_frames_c(self._ctx, dev, C.byref(fb), out_c.n, C.byref(o), sp), "pack_frames_c")
 
-    def set_launch(self, block: int = 512, scan_group: int = 0, blocks_per_cu: int = 4) -> None:
+    def set_launch(self, block: int = 768, scan_group: int = 0, blocks_per_cu: int = 2) -> None:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
         check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")
 

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variants", default="512:0:4,512:8:4,512:4:4,256:0:6,256:8:6")
+    ap.add_argument("--variants", default="768:0:2,512:0:3,512:0:4,256:0:6,512:8:3")
     ap.add_argument("--ablate", default="", help="comma list of INFW_ABLATE codes to time (0 = full kernel)")
     args = ap.parse_args()
     import torch
@@ -39,21 +39,26 @@ def main():
     wl.gen_device(batch, 0, 0)
     res = torch.empty(n, dtype=torch.int32, device=dev)
     ref = None
+    # variant "block:group:blocks_per_cu[:c24log]"; --ablate "a,b" times diagnostic builds instead
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     if args.ablate:
-        variants = [(512, 0, 4, int(a)) for a in args.ablate.split(",")]
+        variants = [(512, 0, 3, int(a)) for a in args.ablate.split(",")]
     times = {v: [] for v in variants}
     s = torch.cuda.current_stream()
     for r in range(args.rounds):
         for v in variants:
             clf.set_launch(*v[:3])
-            if len(v) > 3:
+            if args.ablate:
                 os.environ["INFW_ABLATE"] = str(v[3])
+            elif len(v) > 3:
+                os.environ["INFW_C24LOG"] = str(v[3])
+            else:
+                os.environ.pop("INFW_C24LOG", None)
             clf.classify(batch, results=res)  # warm
             torch.cuda.synchronize()
             if ref is None:
                 ref = res.clone()
-            elif r == 0 and len(v) == 3:
+            elif r == 0 and not args.ablate:
                 assert torch.equal(res, ref), f"variant {v} differs"
             for _ in range(args.iters):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -66,7 +71,8 @@ def main():
     for v in variants:
         med, mn = statistics.median(times[v]), min(times[v])
         out.append({"block": v[0], "scan_group": v[1], "blocks_per_cu": v[2],
-                    "ablate": v[3] if len(v) > 3 else None, "median_ms": round(med, 3),
+                    "ablate": v[3] if args.ablate else None, "c24log": v[3] if len(v) > 3 and not args.ablate else None,
+                    "median_ms": round(med, 3),
                     "min_ms": round(mn, 3), "gpps_median": round(n / med / 1e6, 3)})
         print(json.dumps(out[-1]), flush=True)
 
