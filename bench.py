@@ -205,7 +205,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "traffic_from": traffic_from,
-            "kernel": "classify_kernel<512, 0>" + (" (family-compact layout)" if args.layout == "compact" else ""),
+            "kernel": "classify_kernel<768, 0> (2 workgroups per CU)"
+                      + (" (family-compact layout)" if args.layout == "compact" else ""),
             "kernel_ms_avg": round(avg_kern_ms, 4),
             "algorithmic_bytes_per_packet": round(algo_bytes, 3),
             "layout": args.layout,
