@@ -51,7 +51,7 @@ def stats_from_results(results: np.ndarray, pkt_len: np.ndarray) -> np.ndarray:
 
 
 def check_cfg(cfg: int, n: int, n_prefixes: int = 0, n_templates: int = 0, start: int = 0, device=None,
-              layout: str = "standard"):
+              layout: str = "standard", launch=None):
     """End-to-end parity on one config: device-generated SoA vs host frames + oracle.
     layout "compact": the batch is re-laid out by infw_soa_compact and classified by infw_classify_c."""
     import torch
@@ -61,6 +61,8 @@ def check_cfg(cfg: int, n: int, n_prefixes: int = 0, n_templates: int = 0, start
     clf = infw.Classifier(devices=[device.index or 0], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
     clf.commit()
+    if launch is not None:
+        clf.set_launch(*launch)
     m = oracle_for(wl)
     ores, over, ostats, (hdr, cap, pl, ifx) = oracle_run(m, wl, start, n)
     batch = SoaBatch.empty(n, device)

@@ -523,6 +523,15 @@ def test_compact_layout(cfg, npfx, ntmpl):
     assert np.array_equal(clf.stats_read_all(), wst)
 
 
+@pytest.mark.parametrize("block,group,bpc", [(768, 0, 2), (512, 0, 3), (512, 0, 4), (512, 0, 2), (256, 0, 6),
+                                             (512, 8, 3), (256, 4, 6), (512, 1, 3)])
+def test_launch_shapes(block, group, bpc):
+    """Every launch shape infw_set_launch accepts (decision tables at 16-32 waves per CU, the one-lane-per-rule
+    ballot scan with 1/4/8 packets in flight) gives the oracle's result words and counters."""
+    r = check_cfg(W.CFG2_MIXED_1M, (1 << 17) + 333, 50000, 256, launch=(block, group, bpc))
+    assert_parity(r, f"shape {block}x{bpc} g{group}")
+
+
 def test_classify_host_batches():
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
