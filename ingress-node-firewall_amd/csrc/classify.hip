@@ -257,7 +257,8 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, bool kPrefetch = !(kAblate & 128)>
+          bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
+          bool kPrefetch = !(kAblate & 128)>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -273,6 +274,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     __shared__ unsigned long long s_c24[kCache ? kC24 : 1];
     if (kCache)
         for (int i = threadIdx.x; i < (int)kC24; i += kBlock) s_c24[i] = 0;
+    // per-workgroup LDS cache of single-record IPv6 groups (1 << kB6Log entries of two 16-B halves,
+    // each half carrying the group key: {tag, top, lo} and {tag, top, mid, meta}).  Lanes racing on an
+    // entry may leave halves of two different groups; a reader accepts an entry only when both halves
+    // carry its own key, so it only ever sees one group's record
+    constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
+    __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
+    if (kB6)
+        for (int i = threadIdx.x; i < (int)(2u << kB6Log); i += kBlock) s_b6[i] = u32x4{0u, 0u, 0u, 0u};
     for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) {
         s_pk[i] = 0;
         s_by[i] = 0;
@@ -424,15 +433,34 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     uint64_t w24 = 0, bi = 0;
                     u32x4 bh = {0, 0, 0, 0}, br0 = {0, 0, 0, 0};
+                    uint32_t lng = 0, b6idx = 0;
+                    bool need6 = v6;
+                    uint64_t bhash = 0;
+                    if (v6) bhash = infw_bucket_hash((uint32_t)slot, a32);
+                    if (kB6 && v6) {
+                        b6idx = (uint32_t)(bhash >> 32) >> (32 - kB6Log);
+                        const u32x4 A = s_b6[2 * b6idx], B = s_b6[2 * b6idx + 1];
+                        if (A[0] == (uint32_t)slot + 1 && B[0] == (uint32_t)slot + 1 && A[1] == a32 && B[1] == a32) {
+                            need6 = false;  // the group's one record (kernel view: r0 = {A[2], A[3], B[2], B[3]})
+                            if (infw_rec_match(B[2], (uint64_t)A[3] << 32 | A[2], B[3], infw_bswap32(sw[1]),
+                                               infw_be64(sw[2], sw[3])))
+                                lng = B[3] & 0x1FFFFFFu;
+                        }
+                    }
                     if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
-                    if (v6) {
-                        bi = infw_bucket_hash((uint32_t)slot, a32) & T.bmask;
+                    if (need6) {
+                        bi = bhash & T.bmask;
                         const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
                         bh = b[0];
                         br0 = b[1];
                     }
-                    uint32_t lng = 0;
-                    if (v6) lng = v6_finish(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                    if (need6) {
+                        lng = v6_finish(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                        if (kB6 && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
+                            s_b6[2 * b6idx] = u32x4{bh[0], bh[1], br0[0], br0[1]};
+                            s_b6[2 * b6idx + 1] = u32x4{bh[0], bh[1], br0[2], br0[3]};
+                        }
+                    }
                     if (need24) {
                         sh = d24_value(T, w24, a32);
                         if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
@@ -560,27 +588,28 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault>
+          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog>), dim3(g), dim3(kBlock), 0,
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log>), dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
 
 // The decision-table kernel without sidebands: launch shape (block, resident blocks per CU) and
 // LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.
 template <bool kC>
-bool launch_shape(int block, uint32_t bpc, int log, uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
+bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
                   uint64_t n, uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
     if (block == 512 && bpc == 4 && log == 10) launch<512, 0, 0, false, 8, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 3 && log == 10) launch<512, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6) launch<768, 0, 0, false, 6, false, kC, 12, 9>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 896 && bpc == 2 && log == 12) launch<896, 0, 0, false, 7, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 640 && bpc == 3 && log == 11) launch<640, 0, 0, false, 8, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
@@ -633,8 +662,10 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
     const int env_log = env_l ? atoi(env_l) : 0;
     const int log = env_log ? env_log : (block == 768 ? 12 : bpc <= 3 ? 11 : 10);
     if (group == 0 && !getenv("INFW_ABLATE")) {
-        const bool ok = in_c ? launch_shape<true>(block, bpc, log, cus, T, in, n, results, verdicts, st, stream)
-                             : launch_shape<false>(block, bpc, log, cus, T, in, n, results, verdicts, st, stream);
+        const char *env_b6 = getenv("INFW_B6CACHE");  // tuning: 0 disables the IPv6 group cache
+        const bool b6 = !env_b6 || atoi(env_b6) != 0;
+        const bool ok = in_c ? launch_shape<true>(block, bpc, log, b6, cus, T, in, n, results, verdicts, st, stream)
+                             : launch_shape<false>(block, bpc, log, b6, cus, T, in, n, results, verdicts, st, stream);
         if (ok) return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     if (in_c) {  // any other shape: the compact layout runs 512 x 3
