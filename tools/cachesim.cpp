@@ -215,7 +215,8 @@ int main(int argc, char **argv) {
                hist[2], hist[3], hist[4], hist[5], hist[6], hist[7]);
     }
     for (int lds_entries : {256, 1024, 2048}) {  // per-workgroup direct-mapped LDS cache of tbl24 words
-        const uint32_t wgs = (uint32_t)(n / 131072) ? (uint32_t)(n / 131072) : 1;  // ~131k packets per workgroup, as at 128M packets over 1024 workgroups
+        const uint64_t per_wg = getenv("CACHESIM_WG_PACKETS") ? strtoull(getenv("CACHESIM_WG_PACKETS"), 0, 10) : 131072;
+        const uint32_t wgs = (uint32_t)(n / per_wg) ? (uint32_t)(n / per_wg) : 1;  // ~131k packets per workgroup, as at 128M packets over 1024 workgroups
         std::vector<uint64_t> tag((size_t)wgs * lds_entries, ~0ull);
         uint64_t look = 0, hit = 0;
         for (uint64_t i = 0; i < n; i++) {
@@ -239,7 +240,8 @@ int main(int argc, char **argv) {
     // per-workgroup direct-mapped LDS caches of whole 64-B lines: decision entry lines keyed by
     // (list, class, part) and IPv6 first-probe bucket lines keyed by (slot, /32)
     for (int lines : {64, 128, 256, 512}) {
-        const uint32_t wgs = (uint32_t)(n / 131072) ? (uint32_t)(n / 131072) : 1;
+        const uint64_t per_wg = getenv("CACHESIM_WG_PACKETS") ? strtoull(getenv("CACHESIM_WG_PACKETS"), 0, 10) : 131072;
+        const uint32_t wgs = (uint32_t)(n / per_wg) ? (uint32_t)(n / per_wg) : 1;
         std::vector<uint64_t> etag((size_t)wgs * lines, ~0ull), btag((size_t)wgs * lines, ~0ull);
         uint64_t el = 0, eh = 0, bl = 0, bh = 0;
         for (uint64_t i = 0; i < n; i++) {
