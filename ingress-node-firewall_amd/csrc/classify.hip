@@ -600,7 +600,9 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
 }
 
 // The decision-table kernel without sidebands: launch shape (block, resident blocks per CU) and
-// LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.
+// LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.  Blocks are
+// multiples of 256 threads: other sizes spread their waves unevenly over the 4 SIMDs (measured
+// 640 x 3, 896 x 2, 448 x 4, 384 x 4: 25-40 % slower than 768 x 2).
 template <bool kC>
 bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
                   uint64_t n, uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
@@ -611,10 +613,6 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6) launch<768, 0, 0, false, 6, false, kC, 12, 9>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 896 && bpc == 2 && log == 12) launch<896, 0, 0, false, 7, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 640 && bpc == 3 && log == 11) launch<640, 0, 0, false, 8, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 448 && bpc == 4 && log == 10) launch<448, 0, 0, false, 7, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 384 && bpc == 4 && log == 10) launch<384, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else return false;
     return true;
 }
