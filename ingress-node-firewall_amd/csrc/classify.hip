@@ -608,6 +608,7 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
                   uint64_t n, uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
     if (block == 512 && bpc == 4 && log == 10) launch<512, 0, 0, false, 8, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 3 && log == 10) launch<512, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 512 && bpc == 3 && log == 11 && b6) launch<512, 0, 0, false, 6, false, kC, 11, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
