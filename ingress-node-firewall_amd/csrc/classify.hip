@@ -277,7 +277,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     // per-workgroup LDS cache of single-record IPv6 groups (1 << kB6Log entries of two 16-B halves,
     // each half carrying the group key: {tag, top, lo} and {tag, top, mid, meta}).  Lanes racing on an
     // entry may leave halves of two different groups; a reader accepts an entry only when both halves
-    // carry its own key, so it only ever sees one group's record
+    // carry its own key, so it only ever sees one group's record.  Both LDS caches rely on one lane's
+    // 8- or 16-B access being indivisible: the LDS executes one instruction at a time, and lanes of one
+    // ds_write that hit the same address leave one lane's whole value (every bench run checks 100M
+    // packets of these kernels bit-exactly against the oracle: `gpu_results_bitexact_on_sample`)
     constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
     __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
     if (kB6)
