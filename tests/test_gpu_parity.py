@@ -532,6 +532,63 @@ def test_launch_shapes(block, group, bpc):
     assert_parity(r, f"shape {block}x{bpc} g{group}")
 
 
+def _bucket_hash(slot: int, top: int) -> int:
+    """infw_bucket_hash (csrc/infw_tables.h), for aiming keys at one LDS cache entry."""
+    M = (1 << 64) - 1
+    h = (((slot << 32) | top) * 0x9E3779B97F4A7C15) & M
+    h ^= h >> 31
+    h = (h * 0xBF58476D1CE4E5B9) & M
+    return h ^ (h >> 30)
+
+
+def test_lds_cache_collisions():
+    """The kernel's LDS caches under maximal contention: 64 IPv6 single-record groups that all map to 2 entries of
+    the IPv6 group cache and 64 IPv4 /24s that all map to 2 entries of the word cache, each with its own rule list;
+    packets spread over them, so lanes of one wave keep overwriting the same entries with different groups.  Every
+    result word must still be the oracle's (a torn or mixed entry would answer with another group's list)."""
+    import random
+    import struct
+    import orc
+    from test_incremental_cpu import _packets_for
+    rng = random.Random(11)
+    b6_log, c24_log = 9, 12  # the default shape's cache sizes (768 x 2)
+    want6 = {}
+    while len(want6) < 64:
+        top = rng.getrandbits(32)
+        idx = _bucket_hash(0, top) >> (64 - b6_log)
+        if idx in (3, 77):
+            want6[top] = idx
+    want4 = {}
+    while len(want4) < 64:
+        a24 = rng.getrandbits(24)
+        idx = ((a24 * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - c24_log)  # key = slot << 24 | a24, slot 0
+        if idx in (5, 901):
+            want4[a24] = idx
+    import goenc
+    ents = {}
+    for j, top in enumerate(want6):
+        val = goenc.make_value([{"order": 1 + j % 90, "protocol": "TCP", "ports": "1-60000", "action": "Allow"}])
+        ents[struct.pack("<II", 48 + 32, 1) + top.to_bytes(4, "big") + rng.getrandbits(96).to_bytes(12, "big")] = val
+    for j, a24 in enumerate(want4):
+        val = goenc.make_value([{"order": 1 + (j + 37) % 90, "protocol": "TCP", "ports": "1-60000", "action": "Deny"}])
+        ents[struct.pack("<II", 24 + 32, 1) + (a24 << 8).to_bytes(4, "big") + bytes(12)] = val
+    clf = infw.Classifier(devices=[0], max_entries=len(ents) + 16)
+    m = orc.OracleMap(max_entries=len(ents) + 16)
+    for k, v in ents.items():
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    clf.commit()
+    hdr, cap, pl, ifx = _packets_for(list(ents), rng, 1500)
+    perm = np.random.default_rng(3).permutation(len(ifx))
+    hdr, cap, pl, ifx = hdr[perm], cap[perm], pl[perm], ifx[perm]
+    want, _, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    dev = torch.device("cuda", 0)
+    clf.stats_reset()
+    got, _ = gpu_run(clf, SoaBatch.from_tuples(W.pack_frames(hdr, cap, pl, ifx), dev), len(ifx))
+    assert np.array_equal(got, want)
+    assert np.array_equal(clf.stats_read_all(), wst)
+    assert len(np.unique(want[want != 0])) > 100  # the groups really answer with different lists
+
+
 def test_classify_host_batches():
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
