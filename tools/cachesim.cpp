@@ -127,7 +127,8 @@ int main(int argc, char **argv) {
                             {"parts32x32B", false, false, 32, 32}, {"parts32x16B", false, false, 32, 16},
                             {"parts64x16B", false, false, 64, 16}, {"parts8x32B", false, false, 8, 32},
                             {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 0, 1},
-                            {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1}};
+                            {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1},
+                            {"list_minor", false, false, 0, 64, 64, 0, 0, 2}};
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -380,8 +381,10 @@ int main(int argc, char **argv) {
                 tc[nt++] = {S_ENTRY, 3 * kSpace + (V.entry32 ? (uint64_t)(l1 - 1) * 256 + cls * 32 : ei * V.entry_stride)};
                 const uint64_t slot_i = infw_dt_slot(l1 - 1, cls, val, t.dt_plog2);
                 if (t.dt_plog2) tc[nt - 1].addr = 3 * kSpace + slot_i * 64;  // the compiled layout's entry line
-                if (t.dt_plog2 && V.pairing)
+                if (t.dt_plog2 && V.pairing == 1)
                     tc[nt - 1].addr = 3 * kSpace + (((uint64_t)(l1 - 1) * 16 + (val >> 12)) * 8 + cls) * 64;
+                if (t.dt_plog2 && V.pairing == 2)  // list-minor: (class, part) major, adjacent lists share a line
+                    tc[nt - 1].addr = 3 * kSpace + (((uint64_t)cls * 16 + (val >> 12)) * h.n_lists + (l1 - 1)) * 64;
                 const uint32_t *w = t.dte[slot_i].w;
                 if (w[0] & INFW_DT_ROOT) {
                     const uint64_t li = (w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, val);
