@@ -72,6 +72,7 @@ struct Variant {
     int entry_stride = 64;
     int dense_short = 0;  // 1: short-table lookups touch one 8-B word per matched prefix, prefixes sorted by (slot, address)
     int cuckoo = 0;   // 1: IPv6 groups in the two-choice table above (absent groups touch both buckets)
+    int mini = 0;     // > 0: 16-B mini entry per (list, class, part) holding <= mini segments; others add the 64-B line
     int pairing = 0;  // 1: compiled parts, entry line at ((list * 16 + part) * 8 + cls) * 64 (classes of one part adjacent)
 };
 
@@ -128,7 +129,8 @@ int main(int argc, char **argv) {
                             {"parts64x16B", false, false, 64, 16}, {"parts8x32B", false, false, 8, 32},
                             {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 0, 1},
                             {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1},
-                            {"list_minor", false, false, 0, 64, 64, 0, 0, 2}};
+                            {"list_minor", false, false, 0, 64, 64, 0, 0, 0, 2},
+                            {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3}};
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -385,6 +387,15 @@ int main(int argc, char **argv) {
                     tc[nt - 1].addr = 3 * kSpace + (((uint64_t)(l1 - 1) * 16 + (val >> 12)) * 8 + cls) * 64;
                 if (t.dt_plog2 && V.pairing == 2)  // list-minor: (class, part) major, adjacent lists share a line
                     tc[nt - 1].addr = 3 * kSpace + (((uint64_t)cls * 16 + (val >> 12)) * h.n_lists + (l1 - 1)) * 64;
+                if (t.dt_plog2 && V.mini) {  // mini entry first; the 64-B line only for parts with more segments
+                    const auto &st = seg_starts[ei];
+                    const uint32_t q = val >> 12, lo = q << 12, hi = lo + 4096;
+                    uint32_t nseg = 1;
+                    for (uint32_t x : st) nseg += x > lo && x < hi;
+                    const uint64_t line_addr = tc[nt - 1].addr;
+                    tc[nt - 1] = {S_ENTRY, 6 * kSpace + slot_i * 16};
+                    if (nseg > (uint32_t)V.mini) tc[nt++] = {S_ENTRY, line_addr};
+                }
                 const uint32_t *w = t.dte[slot_i].w;
                 if (w[0] & INFW_DT_ROOT) {
                     const uint64_t li = (w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, val);
