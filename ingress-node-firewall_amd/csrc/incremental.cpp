@@ -79,6 +79,12 @@ void descend(const PendingMap &m, const uint8_t ifx_le[4], uint32_t a, uint32_t 
         leaf(a, v);
         return;
     }
+    // a /8, /16 or /24 block with no entry longer than itself (PendingMap::deeper): every sub-block
+    // answers v — no probes below it
+    if ((L == 8 || L == 16 || L == 24) && !m.has_deeper(L, rd_le32(ifx_le), a)) {
+        for (uint64_t k = 0; k < (1ull << (Lend - L)); k++) leaf(a + (uint32_t)(k << (32 - Lend)), v);
+        return;
+    }
     descend(m, ifx_le, a, L + 1, Lend, v, leaf);
     descend(m, ifx_le, a | (1u << (31 - L)), L + 1, Lend, v, leaf);
 }

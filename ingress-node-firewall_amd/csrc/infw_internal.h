@@ -56,6 +56,18 @@ struct PendingMap {
     // key was not in the committed set).  Drives the incremental commit.
     static constexpr int64_t kAbsent = -1;
     std::unordered_map<NodeKey, int64_t, NodeKeyHash> dirty;
+    // Short-key occupancy below /8, /16 and /24 blocks: (level, ifindex, block bits) -> entries with
+    // 32 or fewer address bits longer than the block.  Lets an incremental commit fill a block that holds
+    // nothing deeper without probing it (a /8 edit: 65536 DIR-24-8 words).
+    std::unordered_map<uint64_t, uint32_t> deeper;
+    static uint64_t deeper_key(uint32_t level, uint32_t ifindex, uint32_t a32) {
+        return (uint64_t)(level >> 3) << 62 | (uint64_t)ifindex << 24 | (a32 >> (32 - level));
+    }
+    void count_deeper(const NodeKey &k, int delta);
+    bool has_deeper(uint32_t level, uint32_t ifindex, uint32_t a32) const {
+        auto it = deeper.find(deeper_key(level, ifindex, a32));
+        return it != deeper.end() && it->second != 0;
+    }
 
     int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
     int remove(const lpm_ip_key_st *key);

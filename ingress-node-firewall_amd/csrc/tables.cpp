@@ -121,10 +121,23 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
     v.vid = pool.intern(val);
     dirty.emplace(k, kAbsent);
     nodes.emplace(k, v);
+    count_deeper(k, +1);
     order.insert(k);
     len_count[k.plen]++;
     generation++;
     return 0;
+}
+
+void PendingMap::count_deeper(const NodeKey &k, int delta) {
+    if (k.plen < 32 || k.plen > 64) return;  // only keys of the short (<= 32 address bits) table
+    const uint32_t L = k.plen - 32, ifx = rd_le32(k.md);
+    const uint32_t a32 = (uint32_t)k.md[4] << 24 | (uint32_t)k.md[5] << 16 | (uint32_t)k.md[6] << 8 | k.md[7];
+    for (uint32_t level : {8u, 16u, 24u}) {
+        if (L <= level) break;
+        uint32_t &c = deeper[deeper_key(level, ifx, a32)];
+        c += (uint32_t)delta;
+        if (c == 0) deeper.erase(deeper_key(level, ifx, a32));
+    }
 }
 
 int PendingMap::remove(const lpm_ip_key_st *key) {
@@ -133,6 +146,7 @@ int PendingMap::remove(const lpm_ip_key_st *key) {
     auto it = nodes.find(k);
     if (it == nodes.end()) return -ENOENT;
     dirty.emplace(k, (int64_t)it->second.vid);
+    count_deeper(it->first, -1);
     nodes.erase(it);
     order.erase(k);
     len_count[k.plen]--;
