@@ -119,7 +119,8 @@ static int run_churn(int n_keys, int seed) {
     if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
     m.dirty.clear();
     int patched = 0, full = 0;
-    for (int round = 0; round < 12; round++) {
+    const int rounds = getenv("ASAN_CHURN_ROUNDS") ? atoi(getenv("ASAN_CHURN_ROUNDS")) : 8;
+    for (int round = 0; round < rounds; round++) {
         const int edits = 1 + rnd() % (round % 3 == 0 ? 400 : 40);
         for (int e = 0; e < edits; e++) {
             const uint32_t r = rnd() % 10;
@@ -159,7 +160,7 @@ static int run_churn(int n_keys, int seed) {
         HostTables f;
         if (compile_tables(m, f, INFW_SHORT_DIR24, 4ull << 30)) return -1;
         const infw_dev_tables tp = h.view(), tf = f.view();
-        for (int i = 0; i < 40000; i++) {
+        for (int i = 0; i < 20000; i++) {
             uint32_t sa[4] = {rnd(), rnd(), rnd(), rnd()};
             if (rnd() % 2 && !keys.empty()) {  // aim at a key's prefix
                 const lpm_ip_key_st &k = keys[rnd() % keys.size()];
@@ -207,7 +208,9 @@ static int check_d24_words() {
 
 int main() {
     int bad = check_d24_words();
-    for (int s = 0; s < 3; s++) bad |= run_churn(3000, s) != 0;
+    // churn seeds: 1 in the CPU test suite, more with ASAN_CHURN_SEEDS (e.g. make asan ASAN_CHURN_SEEDS=3)
+    const int churn_seeds = getenv("ASAN_CHURN_SEEDS") ? atoi(getenv("ASAN_CHURN_SEEDS")) : 1;
+    for (int s = 0; s < churn_seeds; s++) bad |= run_churn(3000, s) != 0;
     const int modes[3] = {INFW_SHORT_DIR24, INFW_SHORT_COMPRESSED, -1};
     for (int s = 0; s < 3; s++)
         for (int mi = 0; mi < 3; mi++) {
