@@ -395,6 +395,31 @@ static int flush_pending(DeviceEpoch &ep, const HostTables &h, uint32_t cus, Pat
     return 0;
 }
 
+// The incremental-commit upload path of a device, warmed up: stream, pinned and device staging, and one
+// DMA copy + one scatter launch (the first of each pays for queue and code-object setup — ~0.1 s — which
+// would otherwise land on the first incremental commit).
+static int make_patch_pipe(Device &d) {
+    DeviceGuard g(d.ordinal);
+    if (!g.ok) return -ENODEV;
+    auto pp = std::make_shared<PatchPipe>();
+    pp->ordinal = d.ordinal;
+    HIP_OK(hipStreamCreateWithFlags(&pp->stream, hipStreamNonBlocking));
+    if (pp->reserve(1u << 20)) {
+        set_error("patch pipe: staging allocation failed");
+        return -ENOMEM;
+    }
+    auto *desc = reinterpret_cast<infw_patch_desc *>(pp->host);
+    *desc = infw_patch_desc{(uint64_t)(uintptr_t)(pp->dev + 512), 0, 16};  // 64 B within the staging buffer
+    HIP_OK(hipMemcpyAsync(pp->dev, pp->host, 256, hipMemcpyHostToDevice, pp->stream));
+    if (infw_launch_scatter(reinterpret_cast<const uint32_t *>(pp->dev + 256), pp->dev, 1, d.cus, pp->stream)) {
+        set_error("patch pipe: warm-up launch failed");
+        return -EIO;
+    }
+    HIP_OK(hipStreamSynchronize(pp->stream));
+    d.patch = pp;
+    return 0;
+}
+
 extern "C" {
 
 const char *infw_last_error(void) { return g_err.c_str(); }
@@ -464,6 +489,8 @@ int infw_create(infw_ctx **out, const int *hip_devices, int n_dev, uint32_t max_
     // an empty epoch so classify works before the first commit (everything misses)
     int rc = infw_table_commit(ctx.get());
     if (rc) return rc;
+    for (auto &d : ctx->devs)
+        if ((rc = make_patch_pipe(d))) return rc;
     ctx->epoch_no = 0;
     ctx->info.epoch = 0;
     *out = ctx.release();
@@ -581,11 +608,8 @@ int infw_table_commit(infw_ctx *ctx) {
                 while (d.spare.use_count() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
                 next = d.spare;
                 if (!d.patch) {
-                    DeviceGuard g(d.ordinal);
-                    auto pp = std::make_shared<PatchPipe>();
-                    pp->ordinal = d.ordinal;
-                    HIP_OK(hipStreamCreateWithFlags(&pp->stream, hipStreamNonBlocking));
-                    d.patch = pp;
+                    rc = make_patch_pipe(d);
+                    if (rc) return rc;
                 }
                 const auto w0 = std::chrono::steady_clock::now();
                 rc = next->order_after_uses(d.patch->stream);  // after the batches that read this image

@@ -20,6 +20,9 @@
 #include <errno.h>
 
 #include <algorithm>
+#include <chrono>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "infw_internal.h"
 
@@ -218,6 +221,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     if (dead_after > 1024 && (uint64_t)dead_after * 2 > n_lists_after) return full("half of the rule lists are unreferenced");
 
     // ---- pass 2: modify the image (nothing below can refuse)
+    const auto tp0 = std::chrono::steady_clock::now();
     const uint32_t n_lists_before = h.n_lists;
     for (uint32_t vid : new_vids) {
         const uint32_t lid = h.n_lists++;
@@ -246,6 +250,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     inc.dead_lists = (uint64_t)dead_after;
     auto list1 = [&](const NodeVal *v) -> uint32_t { return v ? inc.list_of_vid.at(v->vid) + 1 : 0u; };
 
+    const auto tp1 = std::chrono::steady_clock::now();
     // <= /32: shorter prefixes first, so a /25../32 group starts from its final tbl24 word
     std::vector<const Edit *> shorts;
     for (const Edit &e : edits)
@@ -302,6 +307,14 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         }
     }
 
+    const auto tp2 = std::chrono::steady_clock::now();
+    if (getenv("INFW_PATCH_TRACE")) {
+        uint32_t minP = 99;
+        for (const Edit *e : shorts) minP = std::min(minP, e->P);
+        fprintf(stderr, "[patch] %zu edits: lists %.2f ms (%zu new), shorts %.2f ms (%zu, shortest /%u)\n", edits.size(),
+                std::chrono::duration<double, std::milli>(tp1 - tp0).count(), new_vids.size(),
+                std::chrono::duration<double, std::milli>(tp2 - tp1).count(), shorts.size(), minP);
+    }
     // IPv6 buckets
     std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
     for (const auto &kv : inc.slot_of) ifx_of_slot[kv.second] = kv.first;

@@ -804,6 +804,20 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.n_buckets = groups.size();
     }
     if (inc) {
+        // the buffers incremental commits append to get the device images' 25 % slack on the host too, so
+        // the first commits after a compile do not copy a 30-MB vector to grow it by one rule list
+        // (touched once here: a first write into fresh pages can stall for milliseconds in the kernel's
+        // huge-page allocation, which would land on a commit)
+        auto slack = [](auto &v) {
+            const size_t n = v.size();
+            v.resize(n + std::max<size_t>(n / 4, 4096));
+            v.resize(n);
+        };
+        slack(out.tbl8);
+        slack(out.desc);
+        slack(out.rules);
+        slack(out.dte);
+        slack(out.dtl);
         *inc = IncState();
         inc->slot_of = std::move(slot_of);
         inc->list_refs.assign(out.n_lists, 0);
