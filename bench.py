@@ -63,7 +63,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any N, 1 included)
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -96,14 +97,26 @@ def main():
     else:
         algo_bytes = ALGO_BYTES_PER_PKT
     results = torch.empty(n, dtype=torch.int32, device=dev)
-    stats = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # this step's per-rule counters
+    # per-step counters, double-buffered: the RCCL all-reduce of step k (async, on the collective's own
+    # stream) overlaps the classification of step k + 1, and is waited for before step k + 2 reuses its buffer
+    stats_bufs = [torch.zeros((1024, 4), dtype=torch.int64, device=dev) for _ in range(2)]
+    pending = [None, None]
     total = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # job totals (all ranks)
-    clf.stats_bind(0, stats.data_ptr())
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
-    def step(ev=None):
+    def settle(b):
+        if pending[b] is not None:
+            pending[b].wait()            # the launch stream waits for that all-reduce, the host does not
+            total.add_(stats_bufs[b])
+            pending[b] = None
+
+    def step(k, ev=None):
+        b = k & 1
+        settle(b)
+        stats = stats_bufs[b]
         stats.zero_()
+        clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
         if args.layout == "compact":
@@ -112,27 +125,32 @@ def main():
             clf.classify(batch, results=results, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
-            dist.all_reduce(stats)           # RCCL over xGMI: 32 KiB of u64 counters
-        total.add_(stats)
+        if use_dist:
+            pending[b] = dist.all_reduce(stats, async_op=True)  # RCCL over xGMI: 32 KiB of u64 counters
+        else:
+            total.add_(stats)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
+    settle(0)
+    settle(1)
     total.zero_()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step(k, evs[k])
+    settle(0)
+    settle(1)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
@@ -223,7 +241,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     clf.stats_bind(0, None)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
