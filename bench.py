@@ -32,6 +32,48 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md)
 METRIC = "Mpps classified @1M prefixes x 100 rules, 1/2/4/8 GPUs; % HBM BW roofline"
 
 
+class StatsExchange:
+    """Per-step counter blocks (1024 x 4 u64, the stats map of kernel.c:36-41) and their exchange.
+
+    Double-buffered: step k's counters go to buffer k & 1; with use_dist its all-reduce is issued
+    asynchronously (RCCL: on the collective's own stream, so it overlaps step k + 1's classification)
+    and settled — the launch stream waits for it, the host does not — before step k + 2 reuses the
+    buffer, adding the reduced block to `total`.  Without use_dist the block is added directly.
+    tests/test_dist_gloo.py drives this class on gloo with world size 2."""
+
+    def __init__(self, make, use_dist):
+        import torch.distributed as dist
+        self._dist = dist
+        self.bufs = [make(), make()]
+        self.total = make()
+        self.pending = [None, None]
+        self.use_dist = use_dist
+
+    def _settle(self, b):
+        if self.pending[b] is not None:
+            self.pending[b].wait()
+            self.total.add_(self.bufs[b])
+            self.pending[b] = None
+
+    def begin(self, k):
+        """The zeroed counter block step k classifies into."""
+        b = k & 1
+        self._settle(b)
+        self.bufs[b].zero_()
+        return self.bufs[b]
+
+    def end(self, k):
+        b = k & 1
+        if self.use_dist:
+            self.pending[b] = self._dist.all_reduce(self.bufs[b], async_op=True)  # 32 KiB of u64 over xGMI
+        else:
+            self.total.add_(self.bufs[b])
+
+    def drain(self):
+        self._settle(0)
+        self._settle(1)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,25 +139,12 @@ def main():
     else:
         algo_bytes = ALGO_BYTES_PER_PKT
     results = torch.empty(n, dtype=torch.int32, device=dev)
-    # per-step counters, double-buffered: the RCCL all-reduce of step k (async, on the collective's own
-    # stream) overlaps the classification of step k + 1, and is waited for before step k + 2 reuses its buffer
-    stats_bufs = [torch.zeros((1024, 4), dtype=torch.int64, device=dev) for _ in range(2)]
-    pending = [None, None]
-    total = torch.zeros((1024, 4), dtype=torch.int64, device=dev)   # job totals (all ranks)
+    ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
-    def settle(b):
-        if pending[b] is not None:
-            pending[b].wait()            # the launch stream waits for that all-reduce, the host does not
-            total.add_(stats_bufs[b])
-            pending[b] = None
-
     def step(k, ev=None):
-        b = k & 1
-        settle(b)
-        stats = stats_bufs[b]
-        stats.zero_()
+        stats = ex.begin(k)
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
@@ -125,16 +154,12 @@ def main():
             clf.classify(batch, results=results, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        if use_dist:
-            pending[b] = dist.all_reduce(stats, async_op=True)  # RCCL over xGMI: 32 KiB of u64 counters
-        else:
-            total.add_(stats)
+        ex.end(k)
 
     for k in range(args.warmup):
         step(k)
-    settle(0)
-    settle(1)
-    total.zero_()
+    ex.drain()
+    ex.total.zero_()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if use_dist:
         dist.barrier()
@@ -142,8 +167,7 @@ def main():
     ts = time.perf_counter()
     for k in range(args.steps):
         step(k, evs[k])
-    settle(0)
-    settle(1)
+    ex.drain()
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -158,6 +182,7 @@ def main():
     mpps = total_pkts / elapsed / 1e6
     avg_kern_ms = sum(kern_ms) / len(kern_ms)
     achieved = algo_bytes * n / (avg_kern_ms * 1e-3) / 1e9
+    total = ex.total
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
 
     traffic = None

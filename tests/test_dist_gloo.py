@@ -1,7 +1,8 @@
 """Multi-process path on the CPU (gloo, world size 2): each rank classifies its own
-contiguous shard of the global packet index range and the per-rule counters are
-all-reduced — the same sharding and exchange bench.py does over RCCL — and the
-totals equal a single-process run over the whole range.
+contiguous shard of the global packet index range, step by step, and the per-rule
+counters go through bench.py's own StatsExchange (double-buffered asynchronous
+all-reduce, RCCL on the GPU box) — the totals equal a single-process run over the
+whole range.
 
 The per-rank classification here is the product's compiled-table walk on the host
 (infw_debug_walk); on the GPU box the HIP kernel does it (tests/test_gpu_parity.py)."""
@@ -25,7 +26,10 @@ def _free_port():
     return p
 
 
-def _stats_for(start, n):
+STEPS = 4
+
+
+def _classifier():
     import infw
     from infw import workloads as W
     from parity import stats_from_results
@@ -33,19 +37,35 @@ def _stats_for(start, n):
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
     wl.load_into(c)
     c.commit()
-    t = wl.tuples(start, n)
-    return stats_from_results(c.debug_walk(t), t[:, 5])
+
+    def stats_for(start, n):
+        t = wl.tuples(start, n)
+        return stats_from_results(c.debug_walk(t), t[:, 5])
+    return stats_for
+
+
+def _stats_for(start, n):
+    return _classifier()(start, n)
 
 
 def _worker(rank, world, port, out_path):
     sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)),
+                    os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ingress-node-firewall_amd"),
                     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bench import StatsExchange
+    stats_for = _classifier()
     n = N_TOTAL // world
-    st = torch.from_numpy(_stats_for(rank * n, n).view(np.int64).copy())
-    dist.all_reduce(st)                       # bench.py: dist.all_reduce(stats) over RCCL
+    m = n // STEPS
+    ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64), True)
+    for k in range(STEPS):                    # bench.py's step loop: step k = packets [k·m, (k+1)·m) of the shard
+        buf = ex.begin(k)
+        buf.copy_(torch.from_numpy(stats_for(rank * n + k * m, m).view(np.int64)))
+        ex.end(k)
+    ex.drain()
+    st = ex.total
     t = torch.tensor([float(rank + 1)])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py: max-over-ranks timing
     if rank == 0:
