@@ -314,6 +314,10 @@ int main(int argc, char **argv) {
     for (const Variant &V : vars) {
         if (only && !strstr(only, V.name)) continue;
         std::vector<L2> l2(8, L2(4ull << 20));
+        // CACHESIM_PHASES=1: a two-launch split (the whole batch's LPM, then its decision lookups) — the entry
+        // and leaf lines get an L2 of their own instead of sharing it with the LPM lines
+        const bool phases = getenv("CACHESIM_PHASES") && atoi(getenv("CACHESIM_PHASES"));
+        std::vector<L2> l2b(phases ? 8 : 0, L2(4ull << 20));
         uint64_t req[S_N] = {}, miss[S_N] = {};
         for (uint64_t i = 0; i < n; i++) {
             const uint32_t *q = &tup[i * 8];
@@ -405,7 +409,8 @@ int main(int argc, char **argv) {
             L2 &c = l2[(i / 512) % 8];
             for (int k = 0; k < nt; k++) {
                 req[tc[k].s]++;
-                if (!c.access(tc[k].addr)) miss[tc[k].s]++;
+                L2 &ck = phases && (tc[k].s == S_ENTRY || tc[k].s == S_LEAF) ? l2b[(i / 512) % 8] : c;
+                if (!ck.access(tc[k].addr)) miss[tc[k].s]++;
             }
         }
         double tr = 0, tm = 0;
