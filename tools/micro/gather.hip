@@ -39,6 +39,42 @@ __global__ __launch_bounds__(512, 8) void gather(const uint32_t *__restrict__ ta
     out[tid] = acc;
 }
 
+// Spread footprint: `lines` distinct 128-B lines (16 B read from each), one at a random 128-B slot of each
+// `stride`-byte window, so the L2 footprint stays the same while the address span (pages the lookups
+// touch) grows with the stride.
+__global__ __launch_bounds__(512, 8) void gather_spread(const uint32_t *__restrict__ tab, uint32_t lmask, uint32_t stride_w,
+                                                        int iters, uint32_t *__restrict__ out) {
+    const uint32_t tid = blockIdx.x * 512 + threadIdx.x;
+    uint32_t acc = 0, idx = mix(tid);
+    for (int it = 0; it < iters; it++) {
+        const uint32_t l = mix(idx + it * 0x9E3779B9u) & lmask;
+        // a random 128-B slot inside the line's stride window, so the lines spread over all L2 sets
+        const uint32_t slot = (mix(l ^ 0x5bd1e995u) % (stride_w / 32u)) * 32u;
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(tab + (uint64_t)l * stride_w + slot);
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    out[tid] = acc;
+}
+
+void run_spread(const uint32_t *tab, uint64_t fbytes, uint64_t span, uint32_t *out, int grid, int iters) {
+    const uint64_t lines = fbytes / 128, stride = span / lines;
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    gather_spread<<<grid, 512>>>(tab, (uint32_t)(lines - 1), (uint32_t)(stride / 4), iters, out);
+    hipEventRecord(a);
+    const int reps = 5;
+    for (int r = 0; r < reps; r++) gather_spread<<<grid, 512>>>(tab, (uint32_t)(lines - 1), (uint32_t)(stride / 4), iters, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double lookups = (double)grid * 512 * iters * reps;
+    printf("{\"test\": \"spread\", \"footprint_MiB\": %.1f, \"span_MiB\": %.1f, \"stride_B\": %llu, \"Glookups_s\": %.2f}\n",
+           fbytes / 1048576.0, span / 1048576.0, (unsigned long long)stride, lookups / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+}
+
 template <int W, bool kDep>
 void run(const uint32_t *tab, uint64_t tbytes, uint32_t *out, int grid, int iters, const char *name) {
     const uint32_t mask = (uint32_t)(tbytes / W - 1);
@@ -69,6 +105,12 @@ int main(int argc, char **argv) {
     hipMalloc(&tab, max_t);
     hipMemset(tab, 1, max_t);
     hipMalloc(&out, (size_t)grid * 512 * 4);
+    if (argc > 1 && argv[1][0] == 's') {  // "spread": same L2 footprint over a growing address span
+        for (uint64_t f : {2ull << 20, 16ull << 20, 64ull << 20})
+            for (uint64_t span : {(uint64_t)f, (uint64_t)128 << 20, (uint64_t)1 << 30})
+                if (span >= f) run_spread(tab, f, span, out, grid, 64);
+        return 0;
+    }
     if (argc > 1) {  // one configuration (PMC calibration): W=4 or 64, table MiB
         const int w = atoi(argv[1]);
         const uint64_t t = (uint64_t)atoi(argv[2]) << 20;
