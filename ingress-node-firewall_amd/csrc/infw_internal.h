@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <array>
+#include <deque>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -40,7 +41,7 @@ struct NodeVal {
 };
 
 struct ValuePool {
-    std::vector<std::array<uint8_t, 1200>> vals;
+    std::deque<std::array<uint8_t, 1200>> vals;  // deque: growing never copies the values held
     std::unordered_multimap<uint64_t, uint32_t> index;
     uint32_t intern(const uint8_t *v);
 };

@@ -8,6 +8,10 @@
 #include <algorithm>
 #include <numeric>
 #include <queue>
+#include <thread>
+#include <array>
+#include <chrono>
+#include <stdio.h>
 
 #include "infw_internal.h"
 
@@ -61,8 +65,21 @@ void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes) {
     }
 }
 
+// 1200-B value hash, 8 bytes per step (interning 1M distinct values hashes 1.2 GB).
+static uint64_t value_hash(const uint8_t *v) {
+    uint64_t h = 0x84222325CBF29CE4ull;
+    for (size_t i = 0; i < 1200; i += 8) {
+        uint64_t w;
+        memcpy(&w, v + i, 8);
+        h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 32;
+    }
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 29);
+}
+
 uint32_t ValuePool::intern(const uint8_t *v) {
-    uint64_t h = fnv64(v, 1200, 0x84222325CBF29CE4ull);
+    uint64_t h = value_hash(v);
     auto range = index.equal_range(h);
     for (auto it = range.first; it != range.second; ++it)
         if (memcmp(vals[it->second].data(), v, 1200) == 0) return it->second;
@@ -250,6 +267,27 @@ static bool dt_compact_allowed() {
     return !(e && strcmp(e, "wide") == 0);
 }
 
+// Host threads for compiling rule lists (INFW_COMPILE_THREADS overrides; lists are independent, so a
+// compile of 1M distinct 99-rule lists scales with cores).  Small sets stay on the calling thread.
+static int compile_threads(size_t n_items) {
+    if (n_items < 4096) return 1;
+    int t = (int)std::thread::hardware_concurrency();
+    if (const char *e = getenv("INFW_COMPILE_THREADS")) t = atoi(e);
+    return std::max(1, std::min(t, 16));
+}
+
+// f(thread, begin, end) over nt contiguous chunks of [0, n).
+template <class F>
+static void parallel_chunks(size_t n, int nt, F f) {
+    if (nt <= 1) {
+        f(0, 0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) th.emplace_back(f, t, n * (size_t)t / (size_t)nt, n * (size_t)(t + 1) / (size_t)nt);
+    for (auto &x : th) x.join();
+}
+
 int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
                         std::vector<infw_dt_line> &leaves) {
     const uint32_t S = (uint32_t)starts.size();
@@ -387,33 +425,44 @@ static void class_records(const uint8_t *val, std::vector<uint64_t> per[INFW_NCL
 // lists (configs[1]: 10 rules) fits one line per (list, class) — 1/16 of the footprint —
 // while 99-rule lists (configs[2]) need 16 parts to stay at one line per packet.
 static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
-    uint64_t lines[5] = {}, over[5] = {};
-    std::vector<uint64_t> per[INFW_NCLS];
-    std::vector<uint32_t> starts, res;
-    for (const uint8_t *v : vals) {
-        for (auto &p : per) p.clear();
-        class_records(v, per);
-        for (int c = 0; c < INFW_NCLS; c++) {
-            step_function(per[c], starts, res);
-            bool compact = dt_compact_allowed();
-            for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
-            const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
-            for (uint32_t pl = 0; pl <= 4; pl++) {
-                const uint32_t span = 65536u >> pl;
-                uint32_t q = 0, nseg = 1;  // segments of part q: 1 + starts strictly inside it
-                for (size_t k = 1; k < starts.size(); k++) {
-                    while (starts[k] >= (q + 1) * span) {
-                        over[pl] += nseg > segs;
-                        nseg = 1;
-                        q++;
+    const int nt = compile_threads(vals.size());
+    std::vector<std::array<uint64_t, 10>> acc(nt);  // per thread: lines[5], over[5]
+    parallel_chunks(vals.size(), nt, [&](int t, size_t a, size_t b) {
+        uint64_t *lines = acc[t].data(), *over = lines + 5;
+        std::fill(lines, lines + 10, 0ull);
+        std::vector<uint64_t> per[INFW_NCLS];
+        std::vector<uint32_t> starts, res;
+        for (size_t x = a; x < b; x++) {
+            for (auto &p : per) p.clear();
+            class_records(vals[x], per);
+            for (int c = 0; c < INFW_NCLS; c++) {
+                step_function(per[c], starts, res);
+                bool compact = dt_compact_allowed();
+                for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
+                const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
+                for (uint32_t pl = 0; pl <= 4; pl++) {
+                    const uint32_t span = 65536u >> pl;
+                    uint32_t q = 0, nseg = 1;  // segments of part q: 1 + starts strictly inside it
+                    for (size_t k = 1; k < starts.size(); k++) {
+                        while (starts[k] >= (q + 1) * span) {
+                            over[pl] += nseg > segs;
+                            nseg = 1;
+                            q++;
+                        }
+                        nseg += starts[k] > q * span;
                     }
-                    nseg += starts[k] > q * span;
+                    for (; q < (1u << pl); q++, nseg = 1) over[pl] += nseg > segs;
+                    lines[pl] += 1u << pl;
                 }
-                for (; q < (1u << pl); q++, nseg = 1) over[pl] += nseg > segs;
-                lines[pl] += 1u << pl;
             }
         }
-    }
+    });
+    uint64_t lines[5] = {}, over[5] = {};
+    for (const auto &a : acc)
+        for (int pl = 0; pl < 5; pl++) {
+            lines[pl] += a[pl];
+            over[pl] += a[5 + pl];
+        }
     for (uint32_t pl = 0; pl < 4; pl++)
         if (over[pl] * 256 <= lines[pl]) return pl;
     return 4;
@@ -485,7 +534,23 @@ struct ShortEnt {
 };
 }  // namespace
 
+// Capacity for n elements plus the 25 % slack incremental commits append into (compile_tables' inc
+// path), reserved before the buffer is filled so that growing it later needs no copy.
+template <class V>
+static void reserve_slack(V &v, size_t n, bool inc) {
+    v.reserve(inc ? n + std::max<size_t>(n / 4, 4096) : n);
+}
+
 int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uint64_t dir24_budget, IncState *inc) {
+    // INFW_COMPILE_TRACE=1: wall time per phase on stderr
+    const bool trace = getenv("INFW_COMPILE_TRACE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char *what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[compile] %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
     out = HostTables();
     // --- slots: distinct ifindexes, ascending
     std::vector<uint32_t> ifs;
@@ -527,6 +592,8 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         list_of_vid[vid] = lid;
     }
     out.n_lists = (uint32_t)list_of_vid.size();
+    phase("slots+lists");
+    reserve_slack(out.desc, (size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, inc);
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
     // value parts per (list, class): the fewest that keep one table line per packet (choose_dt_plog2),
     // within a 1 GiB budget for the entry lines (INFW_DT_PARTS=1|2|4|8|16 forces one form)
@@ -538,25 +605,65 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > (1ull << 30))
             out.dt_plog2--;
     }
+    phase("choose parts");
     if (const char *e = getenv("INFW_DT_PARTS")) {
         const int v = atoi(e);
         out.dt_plog2 = v == 16 ? 4 : v == 8 ? 3 : v == 4 ? 2 : v == 2 ? 1 : v == 1 ? 0 : out.dt_plog2;
     }
+    reserve_slack(out.dte, ((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS) << out.dt_plog2, inc);
     out.dte.assign(((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS) << out.dt_plog2, infw_dt_line{});
     out.dtl.clear();
     int dt_rc = 0;
     {
-        std::vector<std::pair<uint32_t, uint32_t>> by_lid(list_of_vid.begin(), list_of_vid.end());
-        std::sort(by_lid.begin(), by_lid.end(),
-                  [](const std::pair<uint32_t, uint32_t> &a, const std::pair<uint32_t, uint32_t> &b) {
-                      return a.second < b.second;
-                  });
-        for (auto &p : by_lid)
-            if (!dt_rc)
-                dt_rc = compile_rule_list(m.pool.vals[p.first].data(), out.rules,
-                                          &out.desc[(size_t)p.second * INFW_DESC_STRIDE],
-                                          &out.dte[((size_t)p.second * INFW_NCLS) << out.dt_plog2], out.dtl, out.dt_plog2);
+        // lists in id order, compiled in contiguous id ranges per thread into thread-local rule and leaf
+        // pools; the pools are then concatenated and the chunk's offsets (class-list descriptors, root
+        // entries' leaf index) rebased — the image is identical to a serial compile
+        std::vector<uint32_t> vid_of_lid(out.n_lists);
+        for (const auto &p : list_of_vid) vid_of_lid[p.second] = p.first;
+        const int nt = compile_threads(out.n_lists);
+        std::vector<std::vector<uint64_t>> rules_t(nt);
+        std::vector<std::vector<infw_dt_line>> leaves_t(nt);
+        std::vector<int> rc_t(nt, 0);
+        std::vector<std::pair<size_t, size_t>> range_t(nt);
+        const size_t ents = (size_t)INFW_NCLS << out.dt_plog2;
+        parallel_chunks(out.n_lists, nt, [&](int t, size_t a, size_t b) {
+            range_t[t] = {a, b};
+            for (size_t lid = a; lid < b && !rc_t[t]; lid++)
+                rc_t[t] = compile_rule_list(m.pool.vals[vid_of_lid[lid]].data(), rules_t[t],
+                                            &out.desc[lid * INFW_DESC_STRIDE], &out.dte[lid * ents], leaves_t[t],
+                                            out.dt_plog2);
+        });
+        size_t rbase = 0, lbase = 0;
+        for (int t = 0; t < nt && !dt_rc; t++) {
+            dt_rc = rc_t[t];
+            if (lbase + leaves_t[t].size() > INFW_DT_INDEX) dt_rc = -ENOSPC;
+            if (dt_rc) break;
+            if (t > 0)
+                for (size_t lid = range_t[t].first; lid < range_t[t].second; lid++) {
+                    for (int c = 0; c < INFW_DESC_STRIDE; c++) {
+                        uint64_t &d = out.desc[lid * INFW_DESC_STRIDE + c];
+                        if (d) d += rbase;  // off in the low 32 bits, cnt above
+                    }
+                    for (size_t e = lid * ents; e < (lid + 1) * ents; e++)
+                        if (out.dte[e].w[0] & INFW_DT_ROOT)
+                            out.dte[e].w[0] = INFW_DT_ROOT | (uint32_t)((out.dte[e].w[0] & INFW_DT_INDEX) + lbase);
+                }
+            rbase += rules_t[t].size();
+            lbase += leaves_t[t].size();
+        }
+        if (!dt_rc) {
+            if (rbase >= (1ull << 32)) dt_rc = -ENOSPC;
+            reserve_slack(out.rules, std::max<size_t>(rbase, 1), inc);
+            reserve_slack(out.dtl, std::max<size_t>(lbase, 1), inc);
+            for (int t = 0; t < nt; t++) {
+                out.rules.insert(out.rules.end(), rules_t[t].begin(), rules_t[t].end());
+                std::vector<uint64_t>().swap(rules_t[t]);
+                out.dtl.insert(out.dtl.end(), leaves_t[t].begin(), leaves_t[t].end());
+                std::vector<infw_dt_line>().swap(leaves_t[t]);
+            }
+        }
     }
+    phase("rule lists");
     if (dt_rc) {
         set_error("compile: decision-table leaf pool exceeds 2^31 lines");
         return -ENOSPC;
@@ -589,6 +696,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         }
     }
     out.n_entries = m.nodes.size();
+    phase("split");
 
     // --- short table: per slot, a DIR-24-8 build image (shorter prefixes written
     // first, longer ones overwrite; /25-/32 in 256-entry tbl8 groups) compressed
@@ -695,6 +803,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     if (out.nodes.empty()) out.nodes.push_back(infw_bnode{});
     if (out.vpool.empty()) out.vpool.push_back(0);
 
+    phase("short table");
     // --- long prefixes: levels, markers, best-matching-prefix
     {
         std::vector<uint8_t> lv;
@@ -756,6 +865,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.n_long_entries = set.n;
     }
 
+    phase("long table");
     // --- /32-grouped buckets for IPv6 long prefixes (the fast path)
     {
         struct G {
@@ -803,6 +913,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         }
         out.n_buckets = groups.size();
     }
+    phase("buckets");
     if (inc) {
         // the buffers incremental commits append to get the device images' 25 % slack on the host too, so
         // the first commits after a compile do not copy a 30-MB vector to grow it by one rule list
@@ -825,6 +936,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         inc->list_of_vid = std::move(list_of_vid);
         inc->valid = true;
     }
+    phase("slack+inc");
     return 0;
 }
 

@@ -198,7 +198,10 @@ void build_cfg2(infw_wl &w, Rng &g, uint32_t n, uint32_t n_tmpl) {
         random_addr(g, a, fam);
         uint32_t len = fam == 4 ? v4_len_bgp(g) : v6_len_mix(g);
         push_prefix(w, ifx[g.below(4)], a, len, fam);
-        w.val_index[i] = g.below(n_tmpl);
+        const uint32_t t = g.below(n_tmpl);
+        // distinct-lists variant (n_templates >= n_prefixes): every key carries its own 1200-B value, as
+        // makeIngressFwRulesMap produces one value per key (loader.go:158-161) — no interning in the workload
+        w.val_index[i] = n_tmpl >= n ? i : t;
     }
     zipf_cdf(w.cdf, n, 1.1);
     infw_gen_params &p = w.params;

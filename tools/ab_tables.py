@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--variants", default="base;INFW_DT_FORM=wide")
+    ap.add_argument("--prefixes", type=int, default=0, help="table size (0 = config default)")
+    ap.add_argument("--templates", type=int, default=0,
+                    help="distinct rule lists (0 = config default; >= prefixes: one list per key)")
     ap.add_argument("--launch", action="store_true", help="variants are launch-time settings (one table image)")
     args = ap.parse_args()
     import torch
@@ -35,7 +38,7 @@ def main():
     from infw import workloads as W
     from infw.batch import SoaBatch
     dev = torch.device("cuda", 0)
-    wl = W.Workload(args.cfg)
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
     n = args.batch
     batch = SoaBatch.empty(n, dev)
     wl.gen_device(batch, 0, 0)
@@ -69,7 +72,8 @@ def main():
             wl.load_into(c)
             c.commit()
         info = c.info()
-        print(f"[ab] {v}: {info['device_bytes'] / 2**20:.0f} MiB, compile {info['compile_ms']:.0f} ms",
+        print(f"[ab] {v}: {info['device_bytes'] / 2**20:.0f} MiB, compile {info['compile_ms']:.0f} ms, "
+              f"upload {info['upload_ms']:.0f} ms, lists {info['n_lists']}, parts {info['dt_parts']}",
               file=sys.stderr, flush=True)
         clfs[v] = shared = c
     ref = None
