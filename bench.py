@@ -13,10 +13,18 @@ BASELINE.json configs[2] — 1M mixed IPv4/IPv6 prefixes, BGP-like lengths,
 128M-packet batch per GPU (configs[3]'s 1B-packet job is 8 x 128M).
 Packets are generated on the device from their global index, so a rank's
 shard is identical at any GPU count (weak scaling).
+
+  --global-packets G   configs[3]'s fixed job: G packets in total, rank g of k
+                       takes [g*G/k, (g+1)*G/k) (strong scaling); the line's
+                       stats_digest (SHA-256 of the all-reduced 1024 x 4 u64
+                       counters of one step) is then identical for every k.
+  --templates T        distinct rule lists (T >= prefixes: one 1200-B value per
+                       key, configs[2]'s distinct-lists variant).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -74,6 +82,36 @@ class StatsExchange:
         self._settle(1)
 
 
+def shard_range(global_n, rank, world):
+    """Packets [a, b) of rank `rank` in a fixed job of global_n packets."""
+    return global_n * rank // world, global_n * (rank + 1) // world
+
+
+def stats_digest(block):
+    """SHA-256 of one step's all-reduced counter block: 1024 x {allow pkts, allow bytes, deny pkts, deny bytes}
+    as little-endian u64 (the layout of ruleStatistics_st, ingress_node_firewall.h:45-54)."""
+    import numpy as np
+    a = np.ascontiguousarray(np.asarray(block).astype("<u8").reshape(1024, 4))
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def usable_cores():
+    """Host cores this process may run on: the CPU affinity set, capped by a cgroup v2 CPU quota if any."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def workload_key(cfg, templates, prefixes):
+    """Names the workload a traffic / PMC summary belongs to (profiles/traffic_<key>.json)."""
+    return f"cfg{cfg}" + ("_distinct" if templates and templates >= (prefixes or 1000000) else "")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,11 +120,16 @@ def parse():
     ap.add_argument("--batch", type=int, default=1 << 27, help="packets per GPU per step")
     ap.add_argument("--cfg", type=int, default=2, choices=[1, 2, 4])
     ap.add_argument("--prefixes", type=int, default=0, help="override table size (0 = config default)")
-    ap.add_argument("--cpu-sample", type=int, default=96 << 20,
-                    help="packets in the CPU-baseline sample (~10-15 s of 16-thread oracle work)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--templates", type=int, default=0,
+                    help="distinct rule lists (0 = config default; >= prefixes: one list per key)")
+    ap.add_argument("--global-packets", type=int, default=0,
+                    help="fixed job of this many packets sharded over the ranks (strong scaling, configs[3])")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="packets in the CPU-baseline sample (0: ~10-20 s of oracle work on the usable cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: every usable core)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_cfg2.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (default profiles/traffic_<workload>.json when it matches the kernel)")
     ap.add_argument("--layout", default="standard", choices=["compact", "standard"],
                     help="batch address layout (include/infw.h): 16-B standard (default) or family-compact")
     return ap.parse_args()
@@ -118,27 +161,34 @@ def main():
 
     # ---- tables (host compile, replicated on every GPU)
     t0 = time.time()
-    wl = W.Workload(args.cfg, n_prefixes=args.prefixes)
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
     clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
     t1 = time.time()
     clf.commit()
+    commit_s = time.time() - t1
     info = clf.info()
-    log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries loaded in {t1 - t0:.1f}s, commit {time.time() - t1:.1f}s "
+    log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries loaded in {t1 - t0:.1f}s, commit {commit_s:.1f}s "
         f"(compile {info['compile_ms']:.0f} ms, upload {info['upload_ms']:.0f} ms, "
         f"{info['device_bytes'] / 2**20:.0f} MiB/GPU, lists={info['n_lists']}, levels={info['n_long_levels']})")
 
     # ---- resident input shard, generated on the device by global packet index
-    n = args.batch
-    batch = SoaBatch.empty(n, dev)
-    wl.gen_device(batch, start=rank * n, dev_ordinal=local)
+    if args.global_packets:  # configs[3]: a fixed job, rank g takes [g·N/k, (g+1)·N/k)
+        start, end = shard_range(args.global_packets, rank, world)
+        n = end - start
+    else:                    # weak scaling: a fixed batch per GPU, rank g takes [g·n, (g+1)·n)
+        n = args.batch
+        start = rank * n
+    batch = SoaBatch.empty(max(n, 1), dev).slice(0, n)
+    if n:
+        wl.gen_device(batch, start=start, dev_ordinal=local)
     if args.layout == "compact":  # the packer's production layout (infw_pack_frames_c); converted untimed here
         batch_c = clf.compact(batch, dev=0)
         n6 = int(((batch.meta & 0xFFFF) == 0x86DD).sum().item())
         algo_bytes = 24 + 12 * n6 / n
     else:
         algo_bytes = ALGO_BYTES_PER_PKT
-    results = torch.empty(n, dtype=torch.int32, device=dev)
+    results = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -159,6 +209,11 @@ def main():
     for k in range(args.warmup):
         step(k)
     ex.drain()
+    # the all-reduced counters of one step (every step classifies the same batch): the cross-k invariant
+    digest_block = None
+    if args.warmup:
+        assert not bool((ex.total % args.warmup).any()), "warmup steps' counters differ"
+        digest_block = ex.total // args.warmup
     ex.total.zero_()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if use_dist:
@@ -178,23 +233,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    total_pkts = n * world * args.steps
+    job_pkts = args.global_packets if args.global_packets else n * world
+    total_pkts = job_pkts * args.steps
     mpps = total_pkts / elapsed / 1e6
     avg_kern_ms = sum(kern_ms) / len(kern_ms)
     achieved = algo_bytes * n / (avg_kern_ms * 1e-3) / 1e9
     total = ex.total
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
+    if digest_block is None:
+        assert not bool((total % args.steps).any()), "timed steps' counters differ"
+        digest_block = total // args.steps
+    else:
+        assert torch.equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
+    digest = stats_digest(digest_block.cpu().numpy())
+    block, group, bpc = clf.launch()
+    kernel = f"classify_kernel<{block}, {group}> ({bpc} workgroups per CU)" + (
+        " (family-compact layout)" if args.layout == "compact" else "")
+    wkey = workload_key(args.cfg, args.templates, args.prefixes)
 
     traffic = None
     traffic_from = None
     line_model = None
     extra = {}
-    if os.path.exists(args.traffic_json):
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{wkey}.json")
+    tj = json.load(open(tpath)) if os.path.exists(tpath) else None
+    if tj is not None and (tj.get("kernel") != kernel or tj.get("layout", "standard") != args.layout):
+        log(f"[bench] {tpath} was profiled on {tj.get('kernel')!r} ({tj.get('layout', 'standard')}), not "
+            f"{kernel!r} ({args.layout}): traffic figures omitted")
+        tj = None
+    if tj is not None:
         try:
-            tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_packet", None)
             traffic = None if traffic is None else round(traffic * n)
-            traffic_from = f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this command)"
+            traffic_from = f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {wkey})"
             # random-line model: the kernel's PMC L2 hits/misses per packet priced at the
             # chip's measured random-lookup rates; frac = that bound / the measured kernel time
             r = tj.get("line_rates")
@@ -213,7 +284,7 @@ def main():
                 extra["fetch_size_GBps"] = round(traffic / (avg_kern_ms * 1e-3) / 1e9, 1) if traffic else None
             if "lds_bank_conflict_rate" in tj:
                 extra["lds_bank_conflict_rate"] = round(tj["lds_bank_conflict_rate"], 4)
-        except Exception:
+        except (KeyError, TypeError, ValueError):
             traffic = None
 
     out = {
@@ -225,20 +296,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_packets else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
         "config": {
             "workload": {1: "cfg1: 10k IPv4 /16-/32 prefixes x 10 rules",
                          2: "cfg2: 1M mixed IPv4/IPv6 prefixes (BGP-like lengths) x 99 rules/target, "
-                            "4096 interned lists, 4 ifindexes, Zipf(1.1) sources",
-                         4: "cfg4: adversarial /128 + last-slot ICMPv6"}[args.cfg],
+                            f"{info['n_lists']} " + ("distinct" if wkey.endswith("_distinct") else "interned")
+                            + " lists, 4 ifindexes, Zipf(1.1) sources",
+                         4: "cfg4: adversarial /128 + last-slot ICMPv6"}[args.cfg]
+                        + (f"; configs[3] job of {args.global_packets} packets sharded over {world} GPU(s)"
+                           if args.global_packets else ""),
+            "workload_key": wkey,
             "prefixes": wl.n_entries,
+            "rule_lists": info["n_lists"],
             "packets_per_gpu_per_step": n,
-            "global_batch": n * world,
+            "global_batch": job_pkts,
             "parallelism": f"dp{world} (packet shards, replicated tables, RCCL all-reduce of stats)",
             "packets_counted_in_stats": counted,
+            "stats_digest": digest,
+            "tables": {"device_bytes_per_image": info["device_bytes"], "images_per_gpu": 2,
+                       "dt_parts": info["dt_parts"], "commit_s": round(commit_s, 2),
+                       "compile_ms": round(info["compile_ms"], 1), "upload_ms": round(info["upload_ms"], 1)},
         },
         "roofline": {
             "bound": "hbm",
@@ -248,8 +328,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "traffic_from": traffic_from,
-            "kernel": "classify_kernel<768, 0> (2 workgroups per CU)"
-                      + (" (family-compact layout)" if args.layout == "compact" else ""),
+            "kernel": kernel,
             "kernel_ms_avg": round(avg_kern_ms, 4),
             "algorithmic_bytes_per_packet": round(algo_bytes, 3),
             "layout": args.layout,
@@ -260,8 +339,8 @@ def main():
     }
 
     # ---- CPU baseline: the oracle (plain C restatement of kernel.c) on host cores, rank 0, N=1 only
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, wl, results, n)
+    if world == 1 and rank == 0 and not args.no_cpu_baseline and n:
+        out["cpu_baseline"] = cpu_baseline(args, wl, results, n, start)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -270,21 +349,23 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, wl, results, n):
+def cpu_baseline(args, wl, results, n, start=0):
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
     m = orc.OracleMap(max_entries=wl.n_entries + 16)
     for k, v in wl.entries():
         m.update(k, v)
-    s = min(args.cpu_sample, n)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    cores = usable_cores()
+    threads = args.cpu_threads or cores
+    # ~0.6 Mpps per thread at 1M prefixes: about 15 s of classify work on the usable cores
+    s = min(args.cpu_sample or max(8 << 20, ((threads * 6 << 20) >> 23) << 23), n)
     # bounded sample, in chunks of 8M frame snapshots (80 B each) so host memory stays ~0.7 GB;
     # only the oracle's classify calls are timed (frame synthesis is not CPU-path work)
     secs, parity, chunk, examined, ex_n = 0.0, True, 8 << 20, 0, 0
     for off in range(0, s, chunk):
         c = min(chunk, s - off)
-        hdr, cap, pl, ifx = wl.frames(off, c)
+        hdr, cap, pl, ifx = wl.frames(start + off, c)
         res, _, _, dt = m.classify_frames(hdr, cap, pl, ifx, nthreads=threads)
         secs += dt
         if off == 0:  # the reference's scan work on the first 1M packets (single thread, not timed)
@@ -296,9 +377,12 @@ def cpu_baseline(args, wl, results, n):
     return {
         "value": round(s / secs / 1e6, 3),
         "unit": "Mpps",
-        "cores": threads,
+        "cores": cores,
+        "threads": threads,
+        "affinity_cpus": len(os.sched_getaffinity(0)),
         "kind": "port",
-        "sample": f"first {s} packets of rank 0's cfg{args.cfg} batch, {threads} pthreads, oracle/infw_oracle.c "
+        "sample": f"first {s} packets of rank 0's cfg{args.cfg} batch, {threads} pthreads on {cores} usable cores "
+                  f"(affinity set, cgroup quota), oracle/infw_oracle.c "
                   f"(frame parse + hash-per-length LPM + 100-slot scan), {secs:.2f}s of classify wall time",
         "gpu_results_bitexact_on_sample": parity,
         # bytes of rule records the reference's in-order loop examines per packet (12 B per valid

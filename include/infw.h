@@ -268,6 +268,8 @@ int infw_soa_compact(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, ui
 /* one-lane-per-rule ballot scan with that many packets in flight;           */
 /* blocks_per_cu resident workgroups per CU.                                  */
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
+/* The launch shape infw_classify uses (default or set above; bench reporting). */
+int infw_get_launch(infw_ctx *ctx, int *block, int *scan_group, int *blocks_per_cu);
 
 /* Frame headers -> SoA tuples on the device (the packer of the batch format  */
 /* above, run as a kernel over frames already in HBM).  Asynchronous.          */

@@ -1020,6 +1020,14 @@ int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu)
     return 0;
 }
 
+int infw_get_launch(infw_ctx *ctx, int *block, int *scan_group, int *blocks_per_cu) {
+    if (!ctx || !block || !scan_group || !blocks_per_cu) return -EINVAL;
+    *block = ctx->block;
+    *scan_group = ctx->group;
+    *blocks_per_cu = ctx->blocks_per_cu;
+    return 0;
+}
+
 int infw_stats_read(infw_ctx *ctx, uint32_t rule_id, ruleStatistics_st *per_slot, int *n_slots) {
     if (!ctx || !per_slot) return -EINVAL;
     if (rule_id >= INFW_MAX_TARGETS) return -ENOENT;

@@ -319,22 +319,30 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 // DIR-24-8 word (8 B).  Bits 63..62:
 //   00  plain: list+1 of the whole /24 in bits 0..31;
 //   10  tbl8 group index in bits 0..31 (256 u32 values, one per last byte);
-//   11  inline /24 of <= 3 runs, values <= 0x7FFF: v0 bits 0..14, v1 15..29,
-//       v2 30..44, run starts b1 bits 45..52 and b2 53..60 (b1 <= b2): last
-//       byte x -> x < b1 ? v0 : x < b2 ? v1 : v2.  One 8-B word instead of a
-//       second, dependent L2 request into a tbl8 group.
+//   11  inline /24, one 8-B word instead of a second, dependent L2 request into
+//       a tbl8 group.  Bit 61 picks the form:
+//       0  <= 3 runs, values <= 0x7FFF: v0 bits 0..14, v1 15..29, v2 30..44, run
+//          starts b1 bits 45..52 and b2 53..60 (b1 <= b2): last byte x ->
+//          x < b1 ? v0 : x < b2 ? v1 : v2;
+//       1  two values A, B <= 0x3FFFFF laid out A | B | A (a longer prefix inside
+//          or at either end of its covering /24 — the usual shape): A bits 0..21,
+//          B 22..43, b1 44..51, b2 52..60 (9 bits, 256 = to the end): x in
+//          [b1, b2) ? B : A.  Keeps such /24s inline when list ids exceed 15 bits
+//          (configs[2] with 1M distinct rule lists).
 #define INFW_D24_GROUP (1ull << 63)
 #define INFW_D24_INLINE (1ull << 62)
+#define INFW_D24_ABA (1ull << 61)
 #define INFW_D24_MAXV 0x7FFFu
+#define INFW_D24_ABA_MAXV 0x3FFFFFu
 
 // Word for a /24 whose 256 values are g (tbl8 group gidx): inline when it can be
 // (and allow_inline; 0 keeps every group in tbl8, for A/B measurements).
 INFW_TD uint64_t infw_d24_encode(const uint32_t *g, uint32_t gidx, bool allow_inline = true) {
     uint32_t v[3] = {g[0], 0, 0}, b[2] = {0, 0}, runs = 1;
-    bool ok = allow_inline && g[0] <= INFW_D24_MAXV;
+    bool ok = allow_inline;
     for (uint32_t x = 1; x < 256 && ok; x++) {
         if (g[x] == g[x - 1]) continue;
-        if (runs == 3 || g[x] > INFW_D24_MAXV) ok = false;
+        if (runs == 3) ok = false;
         else {
             b[runs - 1] = x;
             v[runs++] = g[x];
@@ -346,11 +354,22 @@ INFW_TD uint64_t infw_d24_encode(const uint32_t *g, uint32_t gidx, bool allow_in
         v[2] = v[1];
         b[1] = b[0];
     }
-    return INFW_D24_GROUP | INFW_D24_INLINE | (uint64_t)b[1] << 53 | (uint64_t)b[0] << 45 | (uint64_t)v[2] << 30 |
-           (uint64_t)v[1] << 15 | v[0];
+    if (v[0] <= INFW_D24_MAXV && v[1] <= INFW_D24_MAXV && v[2] <= INFW_D24_MAXV)
+        return INFW_D24_GROUP | INFW_D24_INLINE | (uint64_t)b[1] << 53 | (uint64_t)b[0] << 45 | (uint64_t)v[2] << 30 |
+               (uint64_t)v[1] << 15 | v[0];
+    // A | B | A form: two runs (B to the end: b2 = 256), or three whose first and last values agree
+    uint32_t A = v[0], B = v[1], b1 = b[0], b2 = runs == 2 ? 256u : b[1];
+    if (runs == 3 && v[2] != v[0]) return INFW_D24_GROUP | gidx;
+    if (A > INFW_D24_ABA_MAXV || B > INFW_D24_ABA_MAXV) return INFW_D24_GROUP | gidx;
+    return INFW_D24_GROUP | INFW_D24_INLINE | INFW_D24_ABA | (uint64_t)b2 << 52 | (uint64_t)b1 << 44 | (uint64_t)B << 22 |
+           A;
 }
 
 INFW_TD uint32_t infw_d24_inline(uint64_t e, uint32_t x) {
+    if (e & INFW_D24_ABA) {
+        const uint32_t b1 = (uint32_t)(e >> 44) & 0xFFu, b2 = (uint32_t)(e >> 52) & 0x1FFu;
+        return (uint32_t)(e >> (x >= b1 && x < b2 ? 22 : 0)) & INFW_D24_ABA_MAXV;
+    }
     const uint32_t b1 = (uint32_t)(e >> 45) & 0xFFu, b2 = (uint32_t)(e >> 53) & 0xFFu;
     const uint32_t sh = x >= b2 ? 30u : x >= b1 ? 15u : 0u;
     return (uint32_t)(e >> sh) & INFW_D24_MAXV;

@@ -596,13 +596,17 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     reserve_slack(out.desc, (size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, inc);
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
     // value parts per (list, class): the fewest that keep one table line per packet (choose_dt_plog2),
-    // within a 1 GiB budget for the entry lines (INFW_DT_PARTS=1|2|4|8|16 forces one form)
+    // within a budget for the entry lines of one image — 16 GiB by default (INFW_DT_BUDGET_MB): at 1M
+    // distinct 99-rule lists 16 parts take 7.2 GB per image and measured fastest of 1..16 parts
+    // (3.37 vs 3.58 ms at 1 part + leaves, profiles/r02b); INFW_DT_PARTS=1|2|4|8|16 forces one form
     {
         std::vector<const uint8_t *> vals;
         vals.reserve(list_of_vid.size());
         for (const auto &p : list_of_vid) vals.push_back(m.pool.vals[p.first].data());
         out.dt_plog2 = choose_dt_plog2(vals);
-        while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > (1ull << 30))
+        uint64_t budget = 16ull << 30;
+        if (const char *e = getenv("INFW_DT_BUDGET_MB")) budget = strtoull(e, nullptr, 10) << 20;
+        while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > budget)
             out.dt_plog2--;
     }
     phase("choose parts");

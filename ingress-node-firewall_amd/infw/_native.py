@@ -133,6 +133,7 @@ ABI_SYMBOLS = [
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c",
+    "infw_get_launch",
 ]
 
 
@@ -191,6 +192,7 @@ _sig = {
     "infw_table_info": (C.c_int, [C.c_void_p, P(TableInfo)]),
     "infw_debug_walk": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "infw_set_launch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "infw_get_launch": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]),
     "infw_debug_lookup_set": (C.c_int, [C.c_void_p, C.c_uint32]),
     "infw_debug_keys_read": (C.c_int, [C.c_void_p, P(LpmIpKeySt), C.c_uint32, P(C.c_uint32)]),
     "infw_debug_keys_clear": (C.c_int, [C.c_void_p]),

@@ -249,6 +249,12 @@ class Classifier:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
         check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")
 
+    def launch(self) -> Tuple[int, int, int]:
+        """(block, scan_group, blocks_per_cu) infw_classify launches with."""
+        b, g, p = C.c_int(0), C.c_int(0), C.c_int(0)
+        check(N.lib.infw_get_launch(self._ctx, C.byref(b), C.byref(g), C.byref(p)), "get_launch")
+        return b.value, g.value, p.value
+
     # -- statistics map
     def stats_read(self, rule_id: int) -> List[RuleStatisticsSt]:
         """Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt): one entry per device slot."""

@@ -40,6 +40,23 @@ def test_workloads(cfg, npfx, ntmpl):
     walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
 
 
+def test_distinct_lists_parallel_compile(monkeypatch):
+    """configs[2]'s distinct-lists variant (one 1200-B value per key, loader.go:158-161) at 12k keys: the
+    rule lists compile on host threads (>= 4096 lists) into thread-local pools that are rebased; the walk
+    must equal the oracle, and the image must equal a single-threaded compile's (same walk, same counts)."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=12000, n_templates=12000)
+    assert wl.n_templates == 12000 and len(set(wl.val_index().tolist())) == 12000
+    ents = list(wl.entries())
+    c, res = walk_vs_oracle(ents, lambda n, s: wl.frames(s * n, n), n=30000)
+    info = c.info()
+    assert info["n_lists"] >= 11900
+    monkeypatch.setenv("INFW_COMPILE_THREADS", "1")
+    c1, res1 = walk_vs_oracle(ents, lambda n, s: wl.frames(s * n, n), n=30000)
+    i1 = c1.info()
+    for k in ("n_lists", "n_rules", "dt_parts", "n_tbl8_groups"):
+        assert info[k] == i1[k], k
+
+
 def _val(rng, rid_base):
     import goenc
     rules = []

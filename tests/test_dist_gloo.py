@@ -81,3 +81,44 @@ def test_two_rank_shards_allreduce_equal_single_process(tmp_path):
     want = _stats_for(0, N_TOTAL)
     assert np.array_equal(got, want)
     assert got[:, 0].sum() + got[:, 2].sum() > N_TOTAL // 2
+
+
+def _strong_worker(rank, world, port, n_total, out_path):
+    """bench.py --global-packets: rank g classifies [g·N/k, (g+1)·N/k) of one fixed job; the all-reduced
+    counters' digest is what the bench line reports."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)), root, os.path.join(root, "ingress-node-firewall_amd"),
+                    os.path.join(root, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bench import StatsExchange, shard_range, stats_digest
+    stats_for = _classifier()
+    a, b = shard_range(n_total, rank, world)
+    ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64), True)
+    for k in range(2):  # two steps over the same shard, as bench.py repeats its resident batch
+        buf = ex.begin(k)
+        if b > a:
+            buf.copy_(torch.from_numpy(stats_for(a, b - a).view(np.int64)))
+        ex.end(k)
+    ex.drain()
+    assert not bool((ex.total % 2).any())
+    if rank == 0:
+        with open(out_path, "w") as f:
+            f.write(stats_digest((ex.total // 2).numpy()))
+    dist.destroy_process_group()
+
+
+def test_strong_scaling_digest_equal_across_world_sizes(tmp_path):
+    """configs[3]'s invariant: a fixed job's all-reduced per-rule totals are identical at every
+    GPU count — here k = 1, 2, 4 on gloo, with a job size that does not divide evenly — and equal the
+    single-process counters (statistics.go:126-157 sums per-CPU slots the same way)."""
+    from bench import stats_digest
+    n_total = (1 << 15) + 7
+    digests = {}
+    for world in (1, 2, 4):
+        out = str(tmp_path / f"d{world}.txt")
+        mp.start_processes(_strong_worker, args=(world, _free_port(), n_total, out), nprocs=world,
+                           start_method="spawn")
+        digests[world] = open(out).read()
+    assert len(set(digests.values())) == 1, digests
+    assert digests[1] == stats_digest(_stats_for(0, n_total))

@@ -29,6 +29,7 @@ def need_gpu():
     (W.CFG0_DEMO, 1 << 20, 0, 0),            # configs[0]: demo-1 sample on 1M packets
     (W.CFG1_V4_10K, 1 << 20, 0, 0),          # configs[1] table at full size
     (W.CFG2_MIXED_1M, 1 << 19, 100000, 512),  # configs[2] shape, reduced table
+    (W.CFG2_MIXED_1M, 1 << 19, 100000, 100000),  # configs[2] distinct-lists variant: one list per key
     (W.CFG4_ADVERSARIAL, 1 << 19, 20000, 64),
 ])
 def test_parity_configs(cfg, n, npfx, ntmpl):
@@ -118,12 +119,13 @@ def test_epoch_swap_between_batches():
     assert np.array_equal(clf.stats_read_all(), ost_a + ost_b)  # stats persist across swaps
 
 
-def test_full_size_properties():
-    """configs[2] at the bench size (128M packets, full table): size-independent properties —
-    per-rule counters == counters implied by the result words; two runs identical; the first
-    and last 64k packets bit-exact against the oracle."""
+@pytest.mark.parametrize("ntmpl", [0, 1000000])
+def test_full_size_properties(ntmpl):
+    """configs[2] at the bench size (128M packets, full table; ntmpl 1M: the distinct-lists variant, one
+    1200-B value per key): size-independent properties — per-rule counters == counters implied by the
+    result words; two runs identical; the first and last 64k packets bit-exact against the oracle."""
     n = 1 << 27
-    wl = W.Workload(W.CFG2_MIXED_1M)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_templates=ntmpl)
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
     clf.commit()

@@ -202,6 +202,20 @@ static int check_d24_words() {
         for (uint32_t a = 0; a < 256; a++) bad |= infw_dir24_lookup(t, 0, a) != tbl8[a];
         bad |= (runs <= 3 && !big) && (w & INFW_D24_GROUP) && !(w & INFW_D24_INLINE) && tbl8[0] != tbl8[255];
     }
+    // large list ids (configs[2] with 1M distinct lists): the A | B | A form
+    for (int c = 0; c < 20000; c++) {
+        const uint32_t A = rnd() % 0x500000u, B = c % 5 == 0 ? A + 1 : rnd() % 0x500000u;
+        uint32_t b1 = rnd() % 257, b2 = b1 + rnd() % (257 - b1);
+        const int shape = c % 4;  // 0: A B A, 1: A B, 2: B A, 3: A B C (not inlinable when large)
+        if (shape == 1) b2 = 256;
+        if (shape == 2) b1 = 0;
+        for (uint32_t x = 0; x < 256; x++) tbl8[x] = x >= b1 && x < b2 ? B : (shape == 3 && x >= b2 ? A ^ 0x1234u : A);
+        const uint64_t w = infw_d24_encode(tbl8, 0);
+        t.tbl24 = &w;
+        for (uint32_t a = 0; a < 256; a++) bad |= infw_dir24_lookup(t, 0, a) != tbl8[a];
+        const bool aba = shape != 3 || b2 == 256;
+        bad |= aba && A <= INFW_D24_ABA_MAXV && B <= INFW_D24_ABA_MAXV && !(w & INFW_D24_INLINE) && tbl8[0] != tbl8[255];
+    }
     if (bad) printf("d24 word encoding mismatch\n");
     return bad;
 }

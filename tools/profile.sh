@@ -23,9 +23,9 @@ run pmc_fetch --pmc FETCH_SIZE
 run pmc_write --pmc WRITE_SIZE
 run pmc_lds --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES
 run pmc_l2 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
+run pmc_dram --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_sum
 if [ "${PROFILE_DEEP:-0}" = "1" ]; then
   run pmc_sq --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM
-  run pmc_dram --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_sum
   run pmc_tcc --pmc TCC_BUSY_avr TCC_TAG_STALL_sum
 fi
 echo done

@@ -11,7 +11,7 @@ the HBM traffic per launch corrected as MI355X_MICROARCH.md §HBM prescribes:
   bench line), so   read_bytes = FETCH_SIZE*1024 + 0.5 * stream_bytes * n_packets
   (the un-counted half of the stream); gathers are taken at face value
   (64-B requests).  The uncorrected value is kept beside it.
-Also writes profiles/traffic_cfg2.json (bytes per packet) that bench.py reads.
+Also writes profiles/traffic_<workload_key>.json (per-packet figures + kernel) that bench.py reads.
 Usage: tools/summarize_profile.py <tag> [n_packets]
 """
 import collections
@@ -28,20 +28,25 @@ def main():
     tag = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 27
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    # only a configs[2] profile feeds profiles/traffic_cfg2.json (what bench.py reports beside its line)
+    # the profiled command's bench line names the workload (profiles/traffic_<workload_key>.json, which bench.py
+    # reads beside a line of the same workload, kernel and layout)
     bl = [l for l in open(os.path.join(src, "kt.stdout")) if l.startswith("{")] if os.path.exists(
         os.path.join(src, "kt.stdout")) else []
-    is_cfg2 = not bl or json.loads(bl[-1])["config"]["workload"].startswith("cfg2")
+    line = json.loads(bl[-1]) if bl else {}
+    key = line.get("config", {}).get("workload_key", "cfg2")
+    layout = line.get("roofline", {}).get("layout", "standard")
+    if line:
+        n = line["config"]["packets_per_gpu_per_step"]
     stream_b = 32.0  # tuple bytes read per packet
-    if bl and json.loads(bl[-1])["roofline"].get("layout") == "compact":
-        stream_b = json.loads(bl[-1])["roofline"]["algorithmic_bytes_per_packet"] - 4
+    if layout == "compact":
+        stream_b = line["roofline"]["algorithmic_bytes_per_packet"] - 4
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in ("kt/kt_kernel_stats.csv", "kt/kt_domain_stats.csv"):
         p = os.path.join(src, f)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, os.path.basename(p)))
-    out = {"tag": tag, "packets_per_launch": n, "kernels": {}}
+    out = {"tag": tag, "workload_key": key, "packets_per_launch": n, "kernels": {}}
     stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
     for r in stats:
         if "classify" in r["Name"]:
@@ -64,42 +69,30 @@ def main():
         out["hbm_bytes_per_launch"] = corr
         out["hbm_bytes_per_packet"] = corr / n
         out["hbm_bytes_per_packet_raw"] = raw / n
-        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
-        tj = json.load(open(tp)) if os.path.exists(tp) else {}
-        keep = {k: tj[k] for k in ("line_rates",) if k in tj}  # microbenchmark rates outlive a profile
-        json.dump(dict({"tag": tag, "hbm_bytes_per_packet": corr / n, "hbm_bytes_per_packet_raw": raw / n,
-                        "note": "classify kernel, cfg2 bench config; see profiles/%s/summary.json" % tag}, **keep),
-                  open(tp, "w"), indent=1)
     if "TCC_HIT_sum" in avg:
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         out["l2_misses_per_packet"] = avg["TCC_MISS_sum"] / n
         out["l2_hits_per_packet"] = avg["TCC_HIT_sum"] / n
-        tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
-        if os.path.exists(tp):  # the random-line model bench.py reports beside the HBM roofline
-            tj = json.load(open(tp))
-            tj["l2_hits_per_packet"] = out["l2_hits_per_packet"]
-            tj["l2_misses_per_packet"] = out["l2_misses_per_packet"]
-            json.dump(tj, open(tp, "w"), indent=1)
     if "SQ_LDS_BANK_CONFLICT" in avg:
         out["lds_bank_conflict_rate"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"])
     if "TCC_EA0_RDREQ_sum" in avg:  # fabric read requests: one per 128-B line (MI355X_MICROARCH.md §HBM)
         out["ea_rdreq_per_packet"] = avg["TCC_EA0_RDREQ_sum"] / n
-    tp = os.path.join(ROOT, "profiles", "traffic_cfg2.json" if is_cfg2 else f"traffic_{tag}.json")
-    if os.path.exists(tp):
-        tj = json.load(open(tp))
-        for k in ("lds_bank_conflict_rate", "ea_rdreq_per_packet"):
-            if k in out:
-                tj[k] = out[k]
-        json.dump(tj, open(tp, "w"), indent=1)
     if "GRBM_GUI_ACTIVE" in avg and out["kernels"]:
         k = next(iter(out["kernels"].values()))
         out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
-    bench = os.path.join(src, "kt.stdout")
-    if os.path.exists(bench):
-        lines = [l for l in open(bench) if l.startswith("{")]
-        if lines:
-            out["bench_line_under_kernel_trace"] = json.loads(lines[-1])
+    if line:
+        out["bench_line_under_kernel_trace"] = line
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    # the traffic file bench.py reads for this workload: every figure from this one profile
+    if line and "hbm_bytes_per_packet" in out:
+        rates = json.load(open(os.path.join(ROOT, "profiles", "line_rates.json")))
+        tj = {"tag": tag, "workload_key": key, "kernel": line["roofline"]["kernel"], "layout": layout,
+              "note": f"classify kernel, {key} bench command; see profiles/{tag}/summary.json", "line_rates": rates}
+        for k in ("hbm_bytes_per_packet", "hbm_bytes_per_packet_raw", "l2_hits_per_packet", "l2_misses_per_packet",
+                  "lds_bank_conflict_rate", "ea_rdreq_per_packet"):
+            if k in out:
+                tj[k] = out[k]
+        json.dump(tj, open(os.path.join(ROOT, "profiles", f"traffic_{key}.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench_line_under_kernel_trace"}, indent=1))
 
 
