@@ -30,6 +30,8 @@ constexpr int kStatKeys = INFW_MAX_TARGETS;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kIfLds = 256;  // ifindex map entries mirrored in LDS
 constexpr int kC24LogDefault = 10;  // per-workgroup LDS cache of plain DIR-24-8 words: 1 << kC24Log entries
+// word tags of the IPv6 group cache: tag ^ C_j in word j (distinct, so an all-zero entry never validates)
+constexpr uint32_t kB6C0 = 0x00000001u, kB6C1 = 0x5bd1e995u, kB6C2 = 0x9e3779b9u, kB6C3 = 0xc2b2ae35u;
 
 // Short-table lookup through the workgroup's LDS cache of DIR-24-8 words.  Traffic
 // is heavy-tailed (at configs[2] the top 500 of 1M prefixes carry ~65 % of the hits),
@@ -274,13 +276,12 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     __shared__ unsigned long long s_c24[kCache ? kC24 : 1];
     if (kCache)
         for (int i = threadIdx.x; i < (int)kC24; i += kBlock) s_c24[i] = 0;
-    // per-workgroup LDS cache of single-record IPv6 groups (1 << kB6Log entries of two 16-B halves,
-    // each half carrying the group key: {tag, top, lo} and {tag, top, mid, meta}).  Lanes racing on an
-    // entry may leave halves of two different groups; a reader accepts an entry only when both halves
-    // carry its own key, so it only ever sees one group's record.  Both LDS caches rely on one lane's
-    // 8- or 16-B access being indivisible: the LDS executes one instruction at a time, and lanes of one
-    // ds_write that hit the same address leave one lane's whole value (every bench run checks 100M
-    // packets of these kernels bit-exactly against the oracle: `gpu_results_bitexact_on_sample`)
+    // per-workgroup LDS cache of single-record IPv6 groups of slots < 256: 1 << kB6Log entries of four
+    // 8-B words {tag ^ C_j, payload_j}, payloads = the record {lo low, lo high, mid, meta}.  The entry
+    // index and tag are the top bits and the low 32 bits of infw_b6_key(slot, top), a bijection of the
+    // group key, so a word whose tag matches was written for the reader's own group: lanes racing on an
+    // entry, torn at any 8-B granularity, can only leave words of several groups, which fail the check —
+    // no access needs to be indivisible beyond 8 B.  The distinct C_j keep a zeroed entry from validating.
     constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
     __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
     if (kB6)
@@ -436,16 +437,20 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     uint64_t w24 = 0, bi = 0;
                     u32x4 bh = {0, 0, 0, 0}, br0 = {0, 0, 0, 0};
-                    uint32_t lng = 0, b6idx = 0;
+                    uint32_t lng = 0, b6idx = 0, b6tag = 0;
                     bool need6 = v6;
                     uint64_t bhash = 0;
                     if (v6) bhash = infw_bucket_hash((uint32_t)slot, a32);
-                    if (kB6 && v6) {
-                        b6idx = (uint32_t)(bhash >> 32) >> (32 - kB6Log);
+                    const bool b6ok = kB6 && v6 && slot < 256;
+                    if (b6ok) {
+                        const uint64_t bk = infw_b6_key((uint32_t)slot, a32);
+                        b6idx = (uint32_t)(bk >> (40 - kB6Log));
+                        b6tag = (uint32_t)bk;
                         const u32x4 A = s_b6[2 * b6idx], B = s_b6[2 * b6idx + 1];
-                        if (A[0] == (uint32_t)slot + 1 && B[0] == (uint32_t)slot + 1 && A[1] == a32 && B[1] == a32) {
-                            need6 = false;  // the group's one record (kernel view: r0 = {A[2], A[3], B[2], B[3]})
-                            if (infw_rec_match(B[2], (uint64_t)A[3] << 32 | A[2], B[3], infw_bswap32(sw[1]),
+                        if ((A[0] ^ kB6C0) == b6tag && (A[2] ^ kB6C1) == b6tag && (B[0] ^ kB6C2) == b6tag &&
+                            (B[2] ^ kB6C3) == b6tag) {
+                            need6 = false;  // the group's one record r0 = {A[1], A[3], B[1], B[3]}
+                            if (infw_rec_match(B[1], (uint64_t)A[3] << 32 | A[1], B[3], infw_bswap32(sw[1]),
                                                infw_be64(sw[2], sw[3])))
                                 lng = B[3] & 0x1FFFFFFu;
                         }
@@ -459,9 +464,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     if (need6) {
                         lng = v6_finish(T, (uint32_t)slot, a32, sw, bi, bh, br0);
-                        if (kB6 && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
-                            s_b6[2 * b6idx] = u32x4{bh[0], bh[1], br0[0], br0[1]};
-                            s_b6[2 * b6idx + 1] = u32x4{bh[0], bh[1], br0[2], br0[3]};
+                        if (b6ok && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
+                            s_b6[2 * b6idx] = u32x4{b6tag ^ kB6C0, br0[0], b6tag ^ kB6C1, br0[1]};
+                            s_b6[2 * b6idx + 1] = u32x4{b6tag ^ kB6C2, br0[2], b6tag ^ kB6C3, br0[3]};
                         }
                     }
                     if (need24) {

@@ -169,6 +169,19 @@ INFW_TD uint64_t infw_bucket_hash(uint32_t slot, uint32_t top) {
     return h ^ (h >> 30);
 }
 
+// Key of an IPv6 /32 group in the kernel's per-workgroup LDS group cache (slot < 256): a bijection of
+// the 40-bit (slot, top) onto itself.  The entry index is its top bits and every 8-B word of the entry
+// carries its low 32 bits, so (index, word tag) names exactly one group: a word is accepted only when
+// it was written for the reader's own group, whatever the interleaving of writers and readers.
+INFW_TD uint64_t infw_b6_key(uint32_t slot, uint32_t top) {
+    const uint64_t M = (1ull << 40) - 1;
+    uint64_t k = ((uint64_t)slot << 32 | top) & M;
+    k = (k * 0x9E3779B97Full) & M;  // odd multiplier: invertible mod 2^40
+    k ^= k >> 20;                   // xorshift by half the width: invertible
+    k = (k * 0xC2B2AE3D27ull) & M;
+    return k ^ (k >> 23);
+}
+
 // Does record r cover address bits 32..127 (mid, lo)?
 INFW_TD bool infw_rec_match(uint32_t rmid, uint64_t rlo, uint32_t meta, uint32_t mid, uint64_t lo) {
     const uint32_t L = (meta >> 25) + 32;  // 33..128

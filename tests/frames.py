@@ -58,3 +58,16 @@ def snapshots(frames, width: int = 80):
         hdr[i, :b.size] = b
         cap[i] = len(f)
     return hdr, cap, cap.copy()
+
+
+def http_targets(doc, tc):
+    """TestSyncInterfaceIngressRulesWithHTTP (ebpfsyncer_test.go:41-445): (frame, ifindex, expected XDP action) for
+    each connection of a test case — a TCP SYN from the netns peer 192.0.2.{4i+2} to 192.0.2.{4i+1}:port on dummy{i}."""
+    out = []
+    for target, ok in tc["targetResult"].items():
+        ip, port = target.split(":")
+        last = int(ip.split(".")[-1])
+        i = (last - 1) // 4                       # 192.0.2.{4i+1} is dummy{i}
+        peer = f"192.0.2.{4 * i + 2}"
+        out.append((frame(peer, ip, "tcp", int(port)), doc["ifindex"][f"dummy{i}"], 2 if ok else 1))
+    return out

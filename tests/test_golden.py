@@ -2,8 +2,9 @@
 
 Each vector runs through (1) the oracle (pins the oracle) and (2) the
 product's control plane + table compiler on a host-only context, walking the
-compiled GPU table image on the CPU (infw_debug_walk).  The same vectors run
-through the HIP kernel in test_gpu_golden.py.
+compiled GPU table image on the CPU (infw_debug_walk).  The reference's syncer
+vectors run through the HIP kernel in test_gpu_golden.py, the survey probes in
+test_gpu_parity.py (test_survey_probes_on_device).
 """
 import json
 import os
@@ -14,7 +15,7 @@ import pytest
 import goenc
 import infw
 import orc
-from frames import frame, snapshots
+from frames import frame, http_targets, snapshots
 from infw import workloads as W
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -82,18 +83,6 @@ def test_survey_probes_compiled_tables(case):
     # counters implied by the result words equal the probe's counters
     from parity import stats_from_results
     assert np.array_equal(stats_from_results(res, pl), expected_stats(case, frames))
-
-
-def http_targets(doc, tc):
-    """(frame, ifindex, expected XDP action) for each connection of a test case."""
-    out = []
-    for target, ok in tc["targetResult"].items():
-        ip, port = target.split(":")
-        last = int(ip.split(".")[-1])
-        i = (last - 1) // 4                       # 192.0.2.{4i+1} is dummy{i}
-        peer = f"192.0.2.{4 * i + 2}"
-        out.append((frame(peer, ip, "tcp", int(port)), doc["ifindex"][f"dummy{i}"], 2 if ok else 1))
-    return out
 
 
 def test_ebpfsyncer_http_oracle():

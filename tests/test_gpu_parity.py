@@ -543,6 +543,16 @@ def _bucket_hash(slot: int, top: int) -> int:
     return h ^ (h >> 30)
 
 
+def _b6_key(slot: int, top: int) -> int:
+    """infw_b6_key (csrc/infw_tables.h): the IPv6 group cache's 40-bit bijective key (index = its top bits)."""
+    M = (1 << 40) - 1
+    k = ((slot << 32) | top) & M
+    k = (k * 0x9E3779B97F) & M
+    k ^= k >> 20
+    k = (k * 0xC2B2AE3D27) & M
+    return k ^ (k >> 23)
+
+
 def test_lds_cache_collisions():
     """The kernel's LDS caches under maximal contention: 64 IPv6 single-record groups that all map to 2 entries of
     the IPv6 group cache and 64 IPv4 /24s that all map to 2 entries of the word cache, each with its own rule list;
@@ -557,7 +567,7 @@ def test_lds_cache_collisions():
     want6 = {}
     while len(want6) < 64:
         top = rng.getrandbits(32)
-        idx = _bucket_hash(0, top) >> (64 - b6_log)
+        idx = _b6_key(0, top) >> (40 - b6_log)
         if idx in (3, 77):
             want6[top] = idx
     want4 = {}
