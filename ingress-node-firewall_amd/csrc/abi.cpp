@@ -830,6 +830,9 @@ static int make_pipe(int ordinal, uint64_t chunk, std::shared_ptr<HostPipe> &out
     return 0;
 }
 
+static int classify_host_chunks(infw_ctx *ctx, Device &d, const std::shared_ptr<DeviceEpoch> &ep, HostPipe &p,
+                                const infw_batch_soa *in, uint64_t n, uint32_t *results, uint8_t *verdicts);
+
 int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_t n, uint32_t *results,
                        uint8_t *verdicts, uint64_t chunk) {
     if (!ctx || !in) return -EINVAL;
@@ -866,6 +869,25 @@ int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_
     DeviceGuard g(d.ordinal);
     if (!g.ok) return -ENODEV;
     HIP_OK(ep->wait_ready(pipe->run) ? hipErrorUnknown : hipSuccess);
+    int rc = classify_host_chunks(ctx, d, ep, *pipe, in, n, results, verdicts);
+    // also on an error exit: the launches already queued read this epoch, and the copies already queued read from
+    // and write into the caller's host buffers — none may be in flight once this returns
+    ep->mark_use(pipe->run);
+    hipError_t e1 = hipStreamSynchronize(pipe->h2d), e2 = hipStreamSynchronize(pipe->run),
+               e3 = hipStreamSynchronize(pipe->d2h);
+    if (rc) return rc;
+    for (hipError_t e : {e1, e2, e3})
+        if (e != hipSuccess) {
+            set_error(std::string("classify_host: stream synchronize: ") + hipGetErrorString(e));
+            return -EIO;
+        }
+    return 0;
+}
+
+static int classify_host_chunks(infw_ctx *ctx, Device &d, const std::shared_ptr<DeviceEpoch> &ep, HostPipe &p,
+                                const infw_batch_soa *in, uint64_t n, uint32_t *results, uint8_t *verdicts) {
+    HostPipe *pipe = &p;
+    const uint64_t chunk = p.chunk;
     const uint64_t nchunks = (n + chunk - 1) / chunk;
     for (uint64_t k = 0; k < nchunks; k++) {
         HostPipe::Slot &s = pipe->slot[k & 1];
@@ -892,8 +914,6 @@ int infw_classify_host(infw_ctx *ctx, int dev, const infw_batch_soa *in, uint64_
         if (verdicts) HIP_OK(hipMemcpyAsync(verdicts + a, s.ver, c, hipMemcpyDeviceToHost, pipe->d2h));
         HIP_OK(hipEventRecord(s.out_done, pipe->d2h));
     }
-    ep->mark_use(pipe->run);
-    HIP_OK(hipStreamSynchronize(pipe->d2h));
     return 0;
 }
 

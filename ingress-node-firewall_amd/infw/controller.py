@@ -99,8 +99,12 @@ class IngNodeFwController:
         desired = [LpmIpKeySt.from_buffer_copy(k) for k in key_to_rules]
         stale = self.get_stale_keys(desired)
         errs = self.purge_keys(stale)                        # errors logged, not fatal (loader.go:183-186)
-        self.add_or_update_rules(key_to_rules)
-        self.c.commit()                                      # publish as one epoch
+        try:
+            # an update error (e.g. ENOSPC) ends the load (loader.go:187-188), but the reference's per-key map
+            # updates made before it are live: publish them rather than leave them pending for a later commit
+            self.add_or_update_rules(key_to_rules)
+        finally:
+            self.c.commit()                                  # publish as one epoch
         return errs
 
     def get_stale_keys(self, desired: List[LpmIpKeySt]) -> List[LpmIpKeySt]:

@@ -116,6 +116,24 @@ def test_ebpfsyncer_http_product_controller():
         assert list(ver) == [t[2] for t in tg], tc["name"]
 
 
+def test_loader_partial_failure_publishes_applied_updates():
+    """A load that fails part-way (ENOSPC on a full map, loader.go:200-208 returns the error) still publishes the
+    updates made before the failure — the reference's per-key map writes are live at once — instead of leaving them
+    pending for an unrelated later commit."""
+    c = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=2)
+    ctl = infw.IngNodeFwController(c, if_indices=lambda name: [7])
+    deny = [infw.ProtocolRule(order=1, protocol="TCP", ports="80", action="Deny")]
+    with pytest.raises(OSError):
+        ctl.ingress_node_fw_rules_loader({"eth0": [infw.IngressNodeFirewallRules(
+            ["10.0.0.0/8", "11.0.0.0/8", "12.0.0.0/8"], deny)]})
+    assert c.count() == 2
+    frames = [frame(src, proto="tcp", dport=80) for src in ("10.1.2.3", "11.1.2.3", "12.1.2.3")]
+    hdr, cap, pl = snapshots(frames)
+    tuples = W.pack_frames(hdr, cap, pl, np.full(3, 7, np.uint32))
+    ver = infw.verdicts_from_results(c.debug_walk(tuples), tuples[:, 6])
+    assert list(ver) == [1, 1, 2]  # the two applied keys are in the published epoch (XDP_DROP), the third is not
+
+
 def test_ebpfsyncer_key_sets():
     """TestVerifyBPFKeysAfterInterfaceIngressRulesUpdate: the map's key set after each sync."""
     doc = load("ref_ebpfsyncer_keys.json")
