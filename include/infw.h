@@ -310,6 +310,31 @@ int infw_classify_ex(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, ui
                      uint32_t *result_words, uint8_t *xdp_verdicts,
                      const struct infw_classify_ex *ex, void *stream);
 
+/*  - Deny-event payload: the perf sample each record stands for, as the      */
+/*    reader receives it (kernel.c:392-399: bpf_perf_event_output(ctx, map,   */
+/*    BPF_F_CURRENT_CPU | min(len, 256) << 32, &hdr, 8); events.go:77-96       */
+/*    reads perf.Record.RawSample).  Slot k of `samples` belongs to record k    */
+/*    of the event ring: `size` is perf's raw-size field,                       */
+/*    round_up(8 + captured + 4, 8) - 4, and raw[0 .. size) is event_hdr_st,    */
+/*    then the frame's first `captured` bytes, then perf's alignment pad        */
+/*    (written as zeros; the kernel leaves stale ring bytes there).  Frame     */
+/*    bytes past the frame's linear length (XDP multi-buffer frags, which HBM  */
+/*    frames do not carry) are written as zeros.  Bytes past `size` are zero.  */
+#define INFW_EVENT_SAMPLE_BYTES 272   /* 4 + round_up(8 + 256 + 4, 8) - 4       */
+struct infw_event_sample {
+    uint32_t size;
+    uint8_t raw[INFW_EVENT_SAMPLE_BYTES - 4];
+};
+/* Fill samples[k] for k < min(*events_count, events_cap) — the records       */
+/* infw_classify_ex wrote — from the n_frames frames the batch was packed     */
+/* from (record.pkt_index = frame index; a record whose index is >= n_frames  */
+/* gets its header and no frame bytes).  Stream-ordered after the classify: the */
+/* count is read on the device, no host synchronisation.  samples: device     */
+/* memory of events_cap slots.                                                 */
+int infw_events_capture(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n_frames,
+                        const struct infw_event_rec *events, uint64_t events_cap,
+                        const uint64_t *events_count, struct infw_event_sample *samples, void *stream);
+
 /* Host-resident batch: the SoA streams, result words and verdicts live in   */
 /* host memory (as a cgo caller hands them over).  The batch goes through    */
 /* the device in chunks of `chunk` packets (0 = 4M) with three HIP streams:  */

@@ -36,6 +36,10 @@ struct infw_patch_desc {  // patch.hip
 extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, const infw_batch_soa_out *out,
                                        const infw_batch_soa_c_out *out_c, uint32_t cus, hipStream_t stream);
 
+extern "C" int infw_launch_event_samples(const infw_frame_batch *fb, const infw_event_rec *ev, uint64_t cap,
+                                         const uint64_t *count, uint64_t n_frames, infw_event_sample *samples,
+                                         uint32_t cus, hipStream_t stream);
+
 namespace infw {
 
 static thread_local std::string g_err;
@@ -1025,6 +1029,30 @@ int infw_pack_frames_c(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint6
     if (!g.ok) return -ENODEV;
     if (infw_launch_pack_frames(fb, n, nullptr, out, ctx->devs[dev].cus, static_cast<hipStream_t>(stream))) {
         set_error(std::string("pack launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    return 0;
+}
+
+int infw_events_capture(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n_frames,
+                        const infw_event_rec *events, uint64_t events_cap, const uint64_t *events_count,
+                        infw_event_sample *samples, void *stream) {
+    if (!ctx || !fb) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("events_capture: host-only context");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (events_cap && (!events || !events_count || !samples || ((uintptr_t)samples & 7) ||
+                       (n_frames && (!fb->frames || !fb->linear_len || (!fb->offsets && !fb->stride))))) {
+        set_error("events_capture: bad arguments");
+        return -EINVAL;
+    }
+    DeviceGuard g(ctx->devs[dev].ordinal);
+    if (!g.ok) return -ENODEV;
+    if (infw_launch_event_samples(fb, events, events_cap, events_count, n_frames, samples, ctx->devs[dev].cus,
+                                  static_cast<hipStream_t>(stream))) {
+        set_error(std::string("events_capture launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
     return 0;

@@ -96,6 +96,57 @@ extern "C" int infw_launch_pack_frames(const infw_frame_batch *fb, uint64_t n, c
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// Deny-event perf samples (kernel.c:392-399): one wave per ring record, lane l writes bytes [8l, 8l + 8) of the
+// record's 272-B slot {u32 raw size, event_hdr_st, min(len, 256) frame bytes, zero pad}.  Events are a small
+// fraction of a batch, so the byte-granular frame reads (frames sit at arbitrary offsets) are not the cost.
+namespace {
+__global__ __launch_bounds__(256) void event_samples_kernel(const infw_frame_batch fb,
+                                                            const infw_event_rec *__restrict__ ev, uint64_t cap,
+                                                            const uint64_t *__restrict__ count, uint64_t n_frames,
+                                                            uint8_t *__restrict__ out) {
+    static_assert(INFW_EVENT_SAMPLE_BYTES % 8 == 0 && INFW_EVENT_SAMPLE_BYTES / 8 <= 64, "one wave per slot");
+    const uint64_t c = *count;
+    const uint64_t n = c < cap ? c : cap;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += waves) {
+        if (lane >= INFW_EVENT_SAMPLE_BYTES / 8) continue;
+        const infw_event_rec e = ev[r];
+        const uint64_t i = e.pkt_index;
+        const bool in_batch = i < n_frames;  // a record of another batch: header only, no frame read
+        const uint8_t *f = in_batch ? fb.frames + (fb.offsets ? fb.offsets[i] : i * fb.stride) : nullptr;
+        const uint32_t linear = in_batch ? fb.linear_len[i] : 0u;
+        const uint32_t captured = e.captured;
+        const uint32_t size = ((8u + captured + 4u + 7u) & ~7u) - 4u;
+        uint64_t hw;
+        __builtin_memcpy(&hw, &e.hdr, 8);
+        uint64_t w = 0;
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t b = 8 * lane + k;
+            uint32_t v = 0;
+            if (b < 4)
+                v = size >> (8 * b) & 0xFFu;
+            else if (b < 12)
+                v = (uint32_t)(hw >> (8 * (b - 4))) & 0xFFu;
+            else if (b - 12 < captured && b - 12 < linear)
+                v = f[b - 12];
+            w |= (uint64_t)v << (8 * k);
+        }
+        reinterpret_cast<uint64_t *>(out + r * INFW_EVENT_SAMPLE_BYTES)[lane] = w;
+    }
+}
+}  // namespace
+
+extern "C" int infw_launch_event_samples(const infw_frame_batch *fb, const infw_event_rec *ev, uint64_t cap,
+                                         const uint64_t *count, uint64_t n_frames, infw_event_sample *samples,
+                                         uint32_t cus, hipStream_t stream) {
+    if (cap == 0) return 0;
+    const uint64_t blocks = (cap + 3) / 4, lim = 4ull * cus;  // 4 waves (records) per block
+    hipLaunchKernelGGL(event_samples_kernel, dim3((uint32_t)(blocks < lim ? blocks : lim)), dim3(256), 0, stream, *fb,
+                       ev, cap, count, n_frames, reinterpret_cast<uint8_t *>(samples));
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // Standard -> family-compact address layout (infw_batch_soa_c): one lane per packet,
 // packets of a wave = one INFW_V6_GROUP group; an IPv6 lane's rank among the group's
 // IPv6 lanes places its 12 tail bytes.

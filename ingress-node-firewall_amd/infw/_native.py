@@ -109,6 +109,9 @@ class ClassifyEx(C.Structure):
                 ("events_count", C.c_void_p)]
 
 
+EVENT_SAMPLE_BYTES = 272  # INFW_EVENT_SAMPLE_BYTES: u32 perf raw size + raw sample (hdr, <= 256 B, pad)
+
+
 class TableInfo(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("n_entries", C.c_uint64), ("n_if_slots", C.c_uint32),
                 ("n_lists", C.c_uint32), ("n_rules", C.c_uint64), ("n_tbl8_groups", C.c_uint64),
@@ -133,7 +136,7 @@ ABI_SYMBOLS = [
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c",
-    "infw_get_launch",
+    "infw_get_launch", "infw_events_capture",
 ]
 
 
@@ -177,6 +180,8 @@ _sig = {
     "infw_classify_c": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoaC), C.c_uint64, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
     "infw_pack_frames_c": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoaC), C.c_void_p]),
+    "infw_events_capture": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_uint64,
+                                      C.c_void_p, C.c_void_p, C.c_void_p]),
     "infw_soa_compact": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,
                                    C.c_void_p]),
     "infw_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),

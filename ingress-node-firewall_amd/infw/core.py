@@ -245,6 +245,22 @@ class Classifier:
                         out_c.pkt_len.data_ptr(), out_c.meta.data_ptr(), out_c.l4word.data_ptr())
         check(N.lib.infw_pack_frames_c(self._ctx, dev, C.byref(fb), out_c.n, C.byref(o), sp), "pack_frames_c")
 
+    def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
+                       pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
+        """The perf samples of the deny events classify_events wrote (kernel.c:392-399) from the frames the batch was
+        packed from: `samples` is a uint8 tensor of (events capacity) x 272 B (infw_event_sample slots)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        fb = N.FrameBatch(frames.data_ptr(), offsets.data_ptr() if offsets is not None else None, stride,
+                          linear_len.data_ptr(), pkt_len.data_ptr() if pkt_len is not None else None,
+                          ifindex.data_ptr())
+        cap = events.numel() // C.sizeof(N.EventRec)
+        assert samples.numel() >= cap * N.EVENT_SAMPLE_BYTES, "samples: one 272-B slot per event record"
+        check(N.lib.infw_events_capture(self._ctx, dev, C.byref(fb), n_frames, events.data_ptr(), cap,
+                                        events_count.data_ptr(), samples.data_ptr(), sp), "events_capture")
+
     def set_launch(self, block: int = 768, scan_group: int = 0, blocks_per_cu: int = 2) -> None:
         """Launch shape of the classify kernel (tuning knob; see include/infw.h)."""
         check(N.lib.infw_set_launch(self._ctx, block, scan_group, blocks_per_cu), "set_launch")

@@ -557,6 +557,26 @@ uint64_t orc_collect_events(const orc_map *m, const uint8_t *frames, const uint6
     return ne;
 }
 
+/* The perf sample of one DENY event as the reader receives it (perf.Record.RawSample, events.go:64-96):
+ * bpf_perf_event_output(ctx, map, BPF_F_CURRENT_CPU | headerSize << 32, &hdr, sizeof(hdr)) (kernel.c:392-399)
+ * emits a raw record of two fragments — the 8-B event_hdr_st, then headerSize = min(len, MAX_EVENT_DATA) bytes
+ * copied from the start of the XDP frame (bpf_xdp_copy: linear data, then frags) — and the perf core sizes it
+ * round_up(8 + headerSize + sizeof(u32), 8) - sizeof(u32), the tail being alignment pad (perf_prepare_sample).
+ * out (272 B): u32 raw size, raw bytes, zeros after.  Frame bytes past `linear` (frags, which a snapshot of the
+ * linear part does not hold) and the pad are written as zeros.  Returns the raw size. */
+uint32_t orc_perf_sample(const uint8_t *frame, uint32_t linear, const struct orc_event *e, uint8_t *out) {
+    const uint32_t hs = e->captured, size = ((8u + hs + 4u + 7u) & ~7u) - 4u;
+    memset(out, 0, 272);
+    memcpy(out, &size, 4);
+    memcpy(out + 4, &e->ifId, 2);
+    memcpy(out + 6, &e->ruleId, 2);
+    out[8] = e->action;
+    out[9] = e->pad;
+    memcpy(out + 10, &e->pktLength, 2);
+    memcpy(out + 12, frame, hs < linear ? hs : linear);
+    return size;
+}
+
 /* Debug lookup keys (kernel.c:205-216, :291-299): the key each frame would insert
  * into ingress_node_firewall_dbg_map when debug_lookup != 0 — formed after the L4
  * extraction succeeded and before the LPM lookup — in packet order, duplicates

@@ -99,6 +99,9 @@ uint64_t orc_collect_events(const orc_map *m, const uint8_t *frames, const uint6
                             const uint32_t *ifindex, uint64_t n, struct orc_event *events,
                             uint64_t max_events);
 
+/* One event's perf sample (272-B slot: u32 raw size, event_hdr_st, min(len, 256) frame bytes, zero pad). */
+uint32_t orc_perf_sample(const uint8_t *frame, uint32_t linear, const struct orc_event *e, uint8_t *out);
+
 /* Debug lookup keys (24-B lpm_ip_key_st images) in packet order, duplicates included. */
 uint64_t orc_collect_lookup_keys(const uint8_t *frames, const uint64_t *offsets, const uint32_t *caplen,
                                  const uint32_t *pkt_len, const uint32_t *ifindex, uint64_t n,

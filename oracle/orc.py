@@ -35,6 +35,7 @@ _sig = {
                                         C.c_void_p, C.c_uint64]),
     "orc_collect_events": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
+    "orc_perf_sample": (C.c_uint32, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     "orc_collect_lookup_keys": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_uint64, C.c_void_p, C.c_uint64]),
 }
@@ -154,6 +155,28 @@ class OracleMap:
                                     ifx.ctypes.data, n, ev, m)
         return np.array([(e.pkt_index, e.ifId, e.ruleId, e.action, e.pktLength, e.captured) for e in ev[:k]],
                         dtype=np.uint64).reshape(-1, 6)
+
+    def collect_event_samples(self, buf: np.ndarray, offsets: np.ndarray, linear: np.ndarray, pkt_len: np.ndarray,
+                              ifindex: np.ndarray):
+        """DENY events of frames packed back to back in `buf` (frame i at offsets[i], linear[i] bytes) in packet
+        order, and each event's perf sample (kernel.c:392-399): (events as in collect_events, k x 272 uint8)."""
+        n = len(offsets)
+        b = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, np.uint64)
+        cap = np.ascontiguousarray(linear, np.uint32)
+        pl = np.ascontiguousarray(pkt_len, np.uint32)
+        ifx = np.ascontiguousarray(ifindex, np.uint32)
+        ev = (OrcEvent * max(n, 1))()
+        k = _lib.orc_collect_events(self._m, b.ctypes.data, offs.ctypes.data, cap.ctypes.data, pl.ctypes.data,
+                                    ifx.ctypes.data, n, ev, n)
+        out = np.zeros((k, 272), np.uint8)
+        for j in range(k):
+            i = ev[j].pkt_index
+            _lib.orc_perf_sample(b.ctypes.data + int(offs[i]), int(min(cap[i], pl[i])), C.byref(ev[j]),
+                                 out[j].ctypes.data)
+        recs = np.array([(e.pkt_index, e.ifId, e.ruleId, e.action, e.pktLength, e.captured) for e in ev[:k]],
+                        dtype=np.uint64).reshape(-1, 6)
+        return recs, out
 
 
 DBG_MAX_ENTRIES = 16384  # ingress_node_firewall_dbg_map max_entries (kernel.c:63)

@@ -205,6 +205,77 @@ def test_deny_events_match_oracle(cfg, npfx, ntmpl):
     assert all(tuple(r) in wset for r in small.tolist())
 
 
+def event_frames(wl, n_real=20000, seed=11):
+    """Frames for the deny-event payload tests: (a) the generator's 80-B header snapshots of 64k packets at a fixed
+    stride (pkt_len beyond the linear 80 B stands for frags), (b) n_real variable-length real frames back to back
+    (40..300 B) whose IPv4 sources are taken from the generator's IPv4 packets, so most hit a prefix.
+    Each: (buf u8, offsets u64, linear u32, pkt_len u32, ifindex u32, stride or 0)."""
+    from frames import frame
+    rng = np.random.default_rng(seed)
+    hdr, cap, pl, ifx = wl.frames(31337, 1 << 16)
+    v4 = np.nonzero((hdr[:, 12] == 8) & (hdr[:, 13] == 0))[0]
+    fr, fifx = [], []
+    for k in range(n_real):
+        j = int(v4[rng.integers(0, v4.size)])
+        src = "%d.%d.%d.%d" % tuple(int(x) for x in hdr[j, 26:30])
+        fr.append(frame(src, proto=["tcp", "udp", "icmp", "sctp"][k % 4], dport=int(rng.integers(0, 1024)),
+                        icmp_type=int(rng.integers(0, 20)), length=int(rng.integers(40, 300))))
+        fifx.append(int(ifx[j]))
+    offs = np.cumsum([0] + [len(f) for f in fr[:-1]]).astype(np.uint64)
+    lens = np.array([len(f) for f in fr], np.uint32)
+    return [(np.ascontiguousarray(hdr).reshape(-1), np.arange(hdr.shape[0], dtype=np.uint64) * 80,
+             np.minimum(cap, 80).astype(np.uint32), pl, ifx, 80),
+            (np.frombuffer(b"".join(fr), np.uint8), offs, lens, lens.copy(), np.array(fifx, np.uint32), 0)]
+
+
+def test_event_samples():
+    """§8f-1 deny-event payload: frames in HBM -> packer -> classify_events -> infw_events_capture; every perf
+    sample (raw size, event_hdr_st, min(len, 256) frame bytes, pad) bit-exact vs the oracle's, and the consumer's
+    syslog lines (infw/events.py, events.go:77-166) identical for both.  Frames: event_frames() — header snapshots
+    at a fixed stride and variable-length real frames back to back, up to 300 B (256-B captures, and lengths past
+    260 that the consumer rejects)."""
+    import ctypes as C
+    from infw import events as E
+    from infw import _native as N
+    dev = torch.device("cuda", 0)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    names = lambda i: "if%d" % i
+    for buf, offs, lens, plen, fifx, stride in event_frames(wl):
+        n = len(offs)
+        dbuf = torch.from_numpy(np.ascontiguousarray(buf).copy()).to(dev)
+        fkw = dict(stride=stride) if stride else dict(offsets=torch.from_numpy(offs.view(np.int64)).to(dev))
+        batch = SoaBatch.empty(n, dev)
+        clf.pack_frames(dbuf, t(lens), t(fifx), batch, pkt_len=t(plen), **fkw)
+        want_rec, want = m.collect_event_samples(buf, offs, lens, plen, fifx)
+        k = want_rec.shape[0]
+        assert k > 200
+        for cap_ev in (n, 16):  # a ring for every event, and one smaller than the event count
+            ev = torch.zeros(cap_ev * C.sizeof(N.EventRec), dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            clf.classify_events(batch, ev, cnt)
+            smp = torch.full((cap_ev * N.EVENT_SAMPLE_BYTES,), 0xEE, dtype=torch.uint8, device=dev)
+            clf.events_capture(dbuf, t(lens), t(fifx), n, ev, cnt, smp, pkt_len=t(plen), **fkw)
+            torch.cuda.synchronize()
+            assert int(cnt.item()) == k
+            w = min(k, cap_ev)
+            idx = ev.cpu().numpy().view(np.uint64).reshape(-1, 3)[:w, 2]
+            got = smp.cpu().numpy().reshape(-1, N.EVENT_SAMPLE_BYTES)[:w][np.argsort(idx, kind="stable")]
+            if cap_ev == n:
+                assert np.array_equal(got, want)
+                assert E.drain(got, k, names) == E.drain(want, k, names)
+                lines, log = E.drain(want, k, names)
+                assert len(lines) >= 2 * (k - len(log))
+            else:
+                rows = {bytes(r) for r in want}
+                assert all(bytes(r) in rows for r in got)
+                assert E.drain(got, k, names)[1][0] == f"Perf event ring buffer full, dropped {k - 16} samples"
+
+
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""
