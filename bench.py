@@ -132,6 +132,9 @@ def parse():
                     help="PMC traffic summary (default profiles/traffic_<workload>.json when it matches the kernel)")
     ap.add_argument("--layout", default="standard", choices=["compact", "standard"],
                     help="batch address layout (include/infw.h): 16-B standard (default) or family-compact")
+    ap.add_argument("--from-frames", type=int, default=0, metavar="STRIDE",
+                    help="packer-fed step: raw frames resident in HBM at this stride (e.g. 128) -> infw_pack_frames_c "
+                         "-> infw_classify_c, both timed (implies --layout compact)")
     return ap.parse_args()
 
 
@@ -179,10 +182,25 @@ def main():
     else:                    # weak scaling: a fixed batch per GPU, rank g takes [g·n, (g+1)·n)
         n = args.batch
         start = rank * n
-    batch = SoaBatch.empty(max(n, 1), dev).slice(0, n)
-    if n:
-        wl.gen_device(batch, start=start, dev_ordinal=local)
-    if args.layout == "compact":  # the packer's production layout (infw_pack_frames_c); converted untimed here
+    if args.from_frames:
+        args.layout = "compact"
+        stride = args.from_frames
+        frames = torch.empty(max(n, 1) * stride, dtype=torch.uint8, device=dev)
+        f_lin, f_len, f_ifx = (torch.empty(max(n, 1), dtype=torch.int32, device=dev) for _ in range(3))
+        if n:
+            wl.gen_frames_device(frames, stride, f_lin[:n], f_len[:n], f_ifx[:n], start=start, dev_ordinal=local)
+        from infw.batch import SoaBatchC
+        batch_c = SoaBatchC.empty(max(n, 1), dev)
+        batch = None
+    else:
+        batch = SoaBatch.empty(max(n, 1), dev).slice(0, n)
+        if n:
+            wl.gen_device(batch, start=start, dev_ordinal=local)
+    if args.from_frames:  # one untimed pack prices the compact tuple by the batch's IPv6 share
+        clf.pack_frames_c(frames, f_lin[:n], f_ifx[:n], batch_c, pkt_len=f_len[:n], stride=stride)
+        n6 = int(((batch_c.meta[:n] & 0xFFFF) == 0x86DD).sum().item())
+        algo_bytes = 24 + 12 * n6 / n
+    elif args.layout == "compact":  # the packer's production layout (infw_pack_frames_c); converted untimed here
         batch_c = clf.compact(batch, dev=0)
         n6 = int(((batch.meta & 0xFFFF) == 0x86DD).sum().item())
         algo_bytes = 24 + 12 * n6 / n
@@ -198,7 +216,12 @@ def main():
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
-        if args.layout == "compact":
+        if args.from_frames:
+            clf.pack_frames_c(frames, f_lin[:n], f_ifx[:n], batch_c, pkt_len=f_len[:n], stride=stride, stream=stream)
+            if ev is not None:
+                ev[2].record(stream)
+            clf.classify_c(batch_c, results=results, stream=stream)
+        elif args.layout == "compact":
             clf.classify_c(batch_c, results=results, stream=stream)
         else:
             clf.classify(batch, results=results, stream=stream)
@@ -215,7 +238,8 @@ def main():
         assert not bool((ex.total % args.warmup).any()), "warmup steps' counters differ"
         digest_block = ex.total // args.warmup
     ex.total.zero_()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3 if args.from_frames else 2))
+           for _ in range(args.steps)]
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -227,7 +251,11 @@ def main():
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    if args.from_frames:  # ev[0] -> pack -> ev[2] -> classify -> ev[1]
+        pack_ms = [e[0].elapsed_time(e[2]) for e in evs]
+        kern_ms = [e[2].elapsed_time(e[1]) for e in evs]
+    else:
+        kern_ms = [e[0].elapsed_time(e[1]) for e in evs]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -249,7 +277,21 @@ def main():
     block, group, bpc = clf.launch()
     kernel = f"classify_kernel<{block}, {group}> ({bpc} workgroups per CU)" + (
         " (family-compact layout)" if args.layout == "compact" else "")
-    wkey = workload_key(args.cfg, args.templates, args.prefixes)
+    if args.from_frames:
+        # packer: the frame bytes kernel.c reads (ethertype, L3 proto, source address, first L4 word: 11 B IPv4 /
+        # 23 B IPv6) + linear length, frame length, ifindex (12 B) in; the compact tuple (algo_bytes - 4) out
+        s6 = (algo_bytes - 24) / 12
+        pack_bytes = 11 + 12 * s6 + 12 + (algo_bytes - 4)
+        avg_pack = sum(pack_ms) / len(pack_ms)
+        extra_pipe = {"from_frames": {
+            "frame_stride": stride, "pack_kernel_ms_avg": round(avg_pack, 4),
+            "pack_algorithmic_bytes_per_packet": round(pack_bytes, 3),
+            "pack_achieved_GBps": round(pack_bytes * n / (avg_pack * 1e-3) / 1e9, 1),
+            "pipeline_algorithmic_bytes_per_packet": round(pack_bytes + algo_bytes, 3),
+            "pipeline_kernel_ms_avg": round(avg_pack + sum(kern_ms) / len(kern_ms), 4)}}
+    else:
+        extra_pipe = {}
+    wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_frames" if args.from_frames else "")
 
     traffic = None
     traffic_from = None
@@ -303,7 +345,7 @@ def main():
         "config": {
             "workload": {1: "cfg1: 10k IPv4 /16-/32 prefixes x 10 rules",
                          2: "cfg2: 1M mixed IPv4/IPv6 prefixes (BGP-like lengths) x 99 rules/target, "
-                            f"{info['n_lists']} " + ("distinct" if wkey.endswith("_distinct") else "interned")
+                            f"{info['n_lists']} " + ("distinct" if "_distinct" in wkey else "interned")
                             + " lists, 4 ifindexes, Zipf(1.1) sources",
                          4: "cfg4: adversarial /128 + last-slot ICMPv6"}[args.cfg]
                         + (f"; configs[3] job of {args.global_packets} packets sharded over {world} GPU(s)"
@@ -334,6 +376,7 @@ def main():
             "layout": args.layout,
             "random_line_model": line_model,
             **extra,
+            **extra_pipe,
         },
         "cpu_baseline": None,
     }

@@ -1,11 +1,16 @@
 // pack.hip — raw frames in HBM -> SoA header tuples.
 //
-// One lane per frame.  The lane reads only the bytes the XDP program reads
-// (ethertype, L3 proto, source address, first L4 word: kernel.c:104-166,
-// :204, :291) and never a byte at or past the frame's linear length, so
-// frames packed back to back in HBM are safe to read; the tuple is exactly
-// infw_pack_header()'s (infw_pack.h), which the host packer and the generator
-// share.
+// One lane per frame; the tuple is exactly infw_pack_header()'s (infw_pack.h), which the host packer and the
+// generator share: the bytes the XDP program reads (ethertype, L3 proto, source address, first L4 word:
+// kernel.c:104-166, :204, :291), each read as 0 at or past the frame's linear length.
+//
+// Frames sit at a stride or at arbitrary byte offsets, so a lane reading its own frame's bytes would issue ~25
+// byte loads each touching a different cache line per wave.  Instead a wave stages the header window of its 64
+// frames — bytes [10, 58) of each, covered by four 16-B aligned chunks from ((frame + 10) & ~15) — through LDS:
+// in each of four rounds, lanes 4j..4j+3 load the four chunks of one frame (64 contiguous bytes: one request per
+// frame instead of one per byte), then every lane picks its frame's bytes out of LDS.  A chunk is loaded only if
+// it starts before min(linear length, 58): it then holds a byte of the frame, so the aligned 16-B access never
+// leaves the frame's memory (frames packed back to back stay safe to read); chunks not loaded read as zero.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,10 +19,6 @@
 
 namespace {
 
-__device__ __forceinline__ uint32_t byte_at(const uint8_t *f, uint32_t cap, uint32_t off) {
-    return off < cap ? (uint32_t)f[off] : 0u;
-}
-
 struct PackOut {  // standard (saddr) or family-compact (saddr4 + v6tail) address layout
     uint8_t *saddr;
     uint32_t *saddr4;
@@ -25,42 +26,69 @@ struct PackOut {  // standard (saddr) or family-compact (saddr4 + v6tail) addres
     uint32_t *ifindex, *pkt_len, *meta, *l4word;
 };
 
+constexpr uint32_t kWinLo = 10, kWinHi = 58;  // header bytes any tuple field can come from
+constexpr uint32_t kWinWords = 17;             // 64-B window + 4 B: lanes' windows 17 banks apart
+
 template <bool kC>
 __global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch fb, uint64_t n, PackOut out) {
-    // wave-uniform trip count: the compact layout ranks a group's IPv6 lanes with one ballot
+    __shared__ uint32_t win[4][64 * kWinWords];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t *ww = win[wv];
+    // block-uniform trip count (the barriers below); the compact layout ranks a group's IPv6 lanes with one ballot
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
+        const uint64_t wbase = base + 64u * wv;
+        for (uint32_t r = 0; r < 4; r++) {  // round r: chunk (lane & 3) of frame 16r + (lane >> 2)
+            const uint32_t j = 16 * r + (lane >> 2), c = lane & 3u;
+            const uint64_t fi = wbase + j;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (fi < n) {
+                const uint8_t *f = fb.frames + (fb.offsets ? fb.offsets[fi] : fi * fb.stride);
+                const uint32_t lin = fb.linear_len[fi];
+                const uintptr_t first = ((uintptr_t)f + kWinLo) & ~(uintptr_t)15, at = first + 16u * c;
+                if (lin > kWinLo && at < (uintptr_t)f + (lin < kWinHi ? lin : kWinHi))
+                    v = *reinterpret_cast<const uint4 *>(at);
+            }
+            uint32_t *d = ww + j * kWinWords + 4 * c;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+        __syncthreads();
+        const uint64_t i = wbase + lane;
         const bool valid = i < n;
-        uint32_t ethertype = 0, proto = 0, l4off = 0, soff = 0, slen = 0, cap = 0, plen = 0;
-        const uint8_t *f = nullptr;
+        uint32_t ethertype = 0, proto = 0, l4off = 0, soff = 0, slen = 0, cap = 0, plen = 0, d = 0;
         if (valid) {
-            f = fb.frames + (fb.offsets ? fb.offsets[i] : i * fb.stride);
+            const uint8_t *f = fb.frames + (fb.offsets ? fb.offsets[i] : i * fb.stride);
             cap = fb.linear_len[i];
             plen = fb.pkt_len ? fb.pkt_len[i] : cap;
+            d = (uint32_t)(((uintptr_t)f + kWinLo) & 15u);  // the window's byte kWinLo sits at chunk offset d
         }
+        const uint8_t *wb = reinterpret_cast<const uint8_t *>(ww + lane * kWinWords) + d - kWinLo;
+        auto byte_at = [&](uint32_t off) -> uint32_t { return off < cap ? (uint32_t)wb[off] : 0u; };
         if (valid && cap >= 14) {
-            ethertype = byte_at(f, cap, 12) << 8 | byte_at(f, cap, 13);
+            ethertype = byte_at(12) << 8 | byte_at(13);
             if (ethertype == 0x0800) {
-                proto = byte_at(f, cap, 23);
+                proto = byte_at(23);
                 l4off = 34; soff = 26; slen = 4;
             } else if (ethertype == 0x86DD) {
-                proto = byte_at(f, cap, 20);
+                proto = byte_at(20);
                 l4off = 54; soff = 22; slen = 16;
             }
         }
         uint32_t sw[4] = {0, 0, 0, 0};
         for (uint32_t k = 0; k < 16; k++)
-            if (k < slen) sw[k >> 2] |= byte_at(f, cap, soff + k) << (8 * (k & 3));
+            if (k < slen) sw[k >> 2] |= byte_at(soff + k) << (8 * (k & 3));
         uint32_t l4 = 0;
         if (l4off)
-            for (uint32_t k = 0; k < 4; k++) l4 |= byte_at(f, cap, l4off + k) << (8 * k);
+            for (uint32_t k = 0; k < 4; k++) l4 |= byte_at(l4off + k) << (8 * k);
         if (kC) {
             const bool is6 = ethertype == 0x86DD;  // == the meta ethertype the classifier ranks by
             const uint64_t m6 = __ballot(is6);
             if (valid) out.saddr4[i] = sw[0];
             if (is6) {
-                const uint32_t rank = __popcll(m6 & ((1ull << (threadIdx.x & 63u)) - 1));
+                const uint32_t rank = __popcll(m6 & ((1ull << lane) - 1));
                 uint32_t *t = reinterpret_cast<uint32_t *>(out.v6tail + (i >> 6) * (12ull * INFW_V6_GROUP)) + 3 * rank;
                 t[0] = sw[1];
                 t[1] = sw[2];
@@ -75,6 +103,7 @@ __global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch
             out.meta[i] = ethertype | proto << 16 | (cap > 255u ? 255u : cap) << 24;
             out.l4word[i] = l4;
         }
+        __syncthreads();  // the window is rewritten by the next iteration
     }
 }
 

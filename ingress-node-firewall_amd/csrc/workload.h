@@ -48,6 +48,10 @@ int infw_wl_pack(const uint8_t *hdr, const uint32_t *caplen, const uint32_t *pkt
 int infw_wl_upload(infw_wl *wl, int hip_device);
 int infw_wl_gen_soa(infw_wl *wl, uint64_t start, uint64_t n, uint8_t *saddr, uint32_t *ifindex,
                     uint32_t *pkt_len, uint32_t *meta, uint32_t *l4word, void *stream);
+// Device generator of raw frames (an infw_frame_batch at a fixed stride >= INFW_HDR_SNAP): frame i holds the
+// header snapshot infw_wl_frames gives for packet start+i; linear_len = min(linear length, INFW_HDR_SNAP).
+int infw_wl_gen_frames(infw_wl *wl, uint64_t start, uint64_t n, uint8_t *frames, uint64_t stride,
+                       uint32_t *linear_len, uint32_t *pkt_len, uint32_t *ifindex, void *stream);
 
 #ifdef __cplusplus
 }

@@ -316,6 +316,23 @@ __global__ void gen_soa_kernel(infw_gen_params p, uint64_t start, uint64_t n, ui
     }
 }
 
+// Frames of packets [start, start+n) at a fixed stride (AF_XDP-style chunks): the 80-B header snapshot of the
+// host frame builder, the linear length of the snapshot's valid bytes, the frame length, the ifindex.
+__global__ void gen_frames_kernel(infw_gen_params p, uint64_t start, uint64_t n, uint8_t *frames, uint64_t stride,
+                                  uint32_t *linear_len, uint32_t *pkt_len, uint32_t *ifindex) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t h[INFW_HDR_SNAP / 4];
+        uint32_t cap, plen, ifx;
+        infw_gen_header(&p, start + i, reinterpret_cast<uint8_t *>(h), &cap, &plen, &ifx);
+        uint32_t *f = reinterpret_cast<uint32_t *>(frames + i * stride);
+        for (int k = 0; k < INFW_HDR_SNAP / 4; k++) f[k] = h[k];
+        linear_len[i] = cap < INFW_HDR_SNAP ? cap : INFW_HDR_SNAP;
+        pkt_len[i] = plen;
+        ifindex[i] = ifx;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -422,6 +439,21 @@ int infw_wl_gen_soa(infw_wl *w, uint64_t start, uint64_t n, uint8_t *saddr, uint
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(gen_soa_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, p, start, n,
                        reinterpret_cast<uint4 *>(saddr), ifindex, pkt_len, meta, l4word);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int infw_wl_gen_frames(infw_wl *w, uint64_t start, uint64_t n, uint8_t *frames, uint64_t stride,
+                       uint32_t *linear_len, uint32_t *pkt_len, uint32_t *ifindex, void *stream) {
+    if (w->dev < 0) return -ENODEV;
+    if (n == 0) return 0;
+    if (stride < INFW_HDR_SNAP || (stride & 3) || ((uintptr_t)frames & 3)) return -EINVAL;
+    infw_gen_params p = w->params;
+    p.prefixes = w->d_prefixes;
+    p.zipf_cdf = w->cdf.empty() ? nullptr : w->d_cdf;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(gen_frames_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, p, start, n,
+                       frames, stride, linear_len, pkt_len, ifindex);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

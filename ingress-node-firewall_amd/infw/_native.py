@@ -259,6 +259,8 @@ _wsig = {
     "infw_wl_upload": (C.c_int, [C.c_void_p, C.c_int]),
     "infw_wl_gen_soa": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p]),
+    "infw_wl_gen_frames": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 for _name, (_res, _args) in _wsig.items():
     _f = getattr(wl, _name)

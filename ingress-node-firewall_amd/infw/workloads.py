@@ -87,6 +87,21 @@ class Workload:
                                     ifx.ctypes.data, _threads()), "frames")
         return hdr, cap, plen, ifx
 
+    def gen_frames_device(self, frames, stride: int, linear_len, pkt_len, ifindex, start: int, dev_ordinal: int,
+                          stream=None) -> None:
+        """Raw frames of packets [start, start + n) in device memory at a fixed stride (n = linear_len.numel()):
+        frame i = the 80-B header snapshot of frames(); linear_len = min(linear length, 80)."""
+        if self._uploaded != dev_ordinal:
+            N.check(N.wl.infw_wl_upload(self._h, dev_ordinal), "wl upload")
+            self._uploaded = dev_ordinal
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        N.check(N.wl.infw_wl_gen_frames(self._h, start, linear_len.numel(), frames.data_ptr(), stride,
+                                        linear_len.data_ptr(), pkt_len.data_ptr(), ifindex.data_ptr(), sp),
+                "gen_frames")
+
     def tuples(self, start: int, n: int) -> np.ndarray:
         t = np.zeros((n, 8), np.uint32)
         N.check(N.wl.infw_wl_tuples(self._h, start, n, t.ctypes.data, _threads()), "tuples")

@@ -276,6 +276,24 @@ def test_event_samples():
                 assert E.drain(got, k, names)[1][0] == f"Perf event ring buffer full, dropped {k - 16} samples"
 
 
+def test_device_frame_generator():
+    """The bench's frames-in-HBM input (bench.py --from-frames): the device frame generator writes the host frame
+    builder's header snapshots at the stride, and pack -> classify of them equals the oracle on those frames."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=128)
+    dev = torch.device("cuda", 0)
+    n, stride = 5000, 128
+    frames = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    lin, plen, ifx = (torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(3))
+    wl.gen_frames_device(frames, stride, lin, plen, ifx, start=999, dev_ordinal=0)
+    torch.cuda.synchronize()
+    hdr, cap, pl, fx = wl.frames(999, n)
+    f = frames.cpu().numpy().reshape(n, stride)
+    assert np.array_equal(f[:, :80], hdr) and not f[:, 80:].any()
+    assert np.array_equal(lin.cpu().numpy().view(np.uint32), np.minimum(cap, 80))
+    assert np.array_equal(plen.cpu().numpy().view(np.uint32), pl)
+    assert np.array_equal(ifx.cpu().numpy().view(np.uint32), fx)
+
+
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""
