@@ -171,6 +171,8 @@ def main():
     clf.commit()
     commit_s = time.time() - t1
     info = clf.info()
+    import resource
+    peak_rss_gib = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # ru_maxrss: KiB on Linux
     log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries loaded in {t1 - t0:.1f}s, commit {commit_s:.1f}s "
         f"(compile {info['compile_ms']:.0f} ms, upload {info['upload_ms']:.0f} ms, "
         f"{info['device_bytes'] / 2**20:.0f} MiB/GPU, lists={info['n_lists']}, levels={info['n_long_levels']})")
@@ -360,7 +362,9 @@ def main():
             "stats_digest": digest,
             "tables": {"device_bytes_per_image": info["device_bytes"], "images_per_gpu": 2,
                        "dt_parts": info["dt_parts"], "commit_s": round(commit_s, 2),
-                       "compile_ms": round(info["compile_ms"], 1), "upload_ms": round(info["upload_ms"], 1)},
+                       "compile_ms": round(info["compile_ms"], 1), "upload_ms": round(info["upload_ms"], 1),
+                       # peak host RSS of this rank (table compile + workload): N ranks compile side by side
+                       "host_peak_rss_gib": round(peak_rss_gib, 2)},
         },
         "roofline": {
             "bound": "hbm",

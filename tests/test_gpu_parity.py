@@ -390,6 +390,86 @@ def test_survey_probes_on_device(monkeypatch, short_table):
         assert np.array_equal(c.stats_read_all(), expected_stats(case, frames)), case["name"]
 
 
+def test_debug_lookup_capture_compact_layout():
+    """The debug lookup sideband in the family-compact kernels (classify_c: the IPv6 key words come from the
+    v6tail loads): the captured set equals the oracle's dbg map, and results equal the oracle's."""
+    import orc
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 8000
+    batch = SoaBatch.empty(n, dev)
+    wl.gen_device(batch, 4321, 0)
+    hdr, cap, pl, ifx = wl.frames(4321, n)
+    want, n_distinct = orc.debug_map_after(hdr, cap, pl, ifx)
+    assert 1000 < n_distinct < orc.DBG_MAX_ENTRIES
+    bc = clf.compact(batch)
+    clf.debug_lookup(1)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    clf.classify_c(bc, results=res)
+    torch.cuda.synchronize()
+    got = clf.debug_keys()
+    assert len(got) == len(want) and set(got) == set(want)
+    ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=4)
+    assert np.array_equal(res.cpu().numpy().view(np.uint32), ores)
+
+
+def test_multi_device_context():
+    """One context over two device slots (devices=[0, 0]: the path a cgo caller with several GPUs takes, on one
+    card): tables replicated per slot through full and incremental commits, one statistics slot per device
+    summed like per-CPU slots (statistics.go:126-157), debug keys the union of the per-device sets."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=128)
+    clf = infw.Classifier(devices=[0, 0], max_entries=wl.n_entries + 64)
+    assert clf.num_devices == 2
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 1 << 16
+    halves = []
+    for d, start in ((0, 0), (1, n)):
+        b = SoaBatch.empty(n, dev)
+        wl.gen_device(b, start, 0)
+        halves.append((d, start, b))
+    clf.debug_lookup(1)
+    for epoch in range(2):
+        clf.stats_reset()
+        want_stats = np.zeros((1024, 4), np.uint64)
+        for d, start, b in halves:
+            gres, _ = gpu_run(clf, b, n, dev_index=d)
+            hdr, cap, pl, ifx = wl.frames(start, n)
+            ores, _, ost, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+            assert np.array_equal(gres, ores), (epoch, d)
+            want_stats += ost
+            slots = clf.stats_read(1)
+            assert len(slots) == 2
+        assert np.array_equal(clf.stats_read_all(), want_stats)
+        per_slot = [clf.stats_read(r) for r in range(1, 100)]
+        assert all(s[0].allow_packets + s[1].allow_packets == want_stats[r + 1, 0] for r, s in enumerate(per_slot))
+        if epoch == 0:  # an incremental commit: delete every 4th key, rewrite every 7th
+            keys = wl.keys_bytes().reshape(-1, 24)
+            tmpl = wl.templates_bytes().reshape(-1, 1200)
+            for i in range(0, keys.shape[0], 4):
+                kb = keys[i].tobytes()
+                assert clf.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb)) == m.delete(kb)
+            for i in range(1, keys.shape[0], 7):
+                kb, vb = keys[i].tobytes(), tmpl[(i * 3) % tmpl.shape[0]].tobytes()
+                assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb),
+                                     infw.RulesValSt.from_buffer_copy(vb)) == m.update(kb, vb)
+            clf.commit()
+            assert clf.info()["commit_mode"] == 1  # INFW_COMMIT_INCREMENTAL, applied to both device slots
+    import orc
+    allk = set()
+    for d, start, b in halves:
+        hdr, cap, pl, ifx = wl.frames(start, n)
+        allk |= set(orc.debug_map_after(hdr, cap, pl, ifx, max_entries=2 * n)[0])
+    got = clf.debug_keys()
+    assert len(got) == len(set(got)) == min(len(allk), orc.DBG_MAX_ENTRIES) and set(got) <= allk
+
+
 def test_debug_lookup_capture():
     """§8f-4 debug lookup capture (kernel.c:59-64, :214-216, :297-299): with debug_lookup set, the set of
     lookup keys equals the oracle's dbg map (first-seen NOEXIST inserts, <= 16384 keys); repeats leave it
