@@ -122,6 +122,8 @@ def parse():
     ap.add_argument("--prefixes", type=int, default=0, help="override table size (0 = config default)")
     ap.add_argument("--templates", type=int, default=0,
                     help="distinct rule lists (0 = config default; >= prefixes: one list per key)")
+    ap.add_argument("--uniform", action="store_true",
+                    help="sources uniform over the prefixes instead of the config's Zipf(1.1) (cache-hostile variant)")
     ap.add_argument("--global-packets", type=int, default=0,
                     help="fixed job of this many packets sharded over the ranks (strong scaling, configs[3])")
     ap.add_argument("--cpu-sample", type=int, default=0,
@@ -165,6 +167,8 @@ def main():
     # ---- tables (host compile, replicated on every GPU)
     t0 = time.time()
     wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
+    if args.uniform:
+        wl.uniform_sources()
     clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
     t1 = time.time()
@@ -293,7 +297,8 @@ def main():
             "pipeline_kernel_ms_avg": round(avg_pack + sum(kern_ms) / len(kern_ms), 4)}}
     else:
         extra_pipe = {}
-    wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_frames" if args.from_frames else "")
+    wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_uniform" if args.uniform else "") + (
+        "_frames" if args.from_frames else "")
 
     traffic = None
     traffic_from = None
@@ -348,7 +353,7 @@ def main():
             "workload": {1: "cfg1: 10k IPv4 /16-/32 prefixes x 10 rules",
                          2: "cfg2: 1M mixed IPv4/IPv6 prefixes (BGP-like lengths) x 99 rules/target, "
                             f"{info['n_lists']} " + ("distinct" if "_distinct" in wkey else "interned")
-                            + " lists, 4 ifindexes, Zipf(1.1) sources",
+                            + " lists, 4 ifindexes, " + ("uniform" if args.uniform else "Zipf(1.1)") + " sources",
                          4: "cfg4: adversarial /128 + last-slot ICMPv6"}[args.cfg]
                         + (f"; configs[3] job of {args.global_packets} packets sharded over {world} GPU(s)"
                            if args.global_packets else ""),

@@ -30,6 +30,8 @@ uint32_t infw_wl_n_templates(const infw_wl *wl);
 const struct rulesVal_st *infw_wl_templates(const infw_wl *wl);
 // Host-side generator parameters (pointers into wl).
 const struct infw_gen_params *infw_wl_params(const infw_wl *wl);
+// Sources drawn uniformly over the prefixes instead of the config's Zipf law (tables unchanged).
+void infw_wl_uniform_sources(infw_wl *wl);
 // Overwrite the packet seed (tables unchanged).
 void infw_wl_set_packet_seed(infw_wl *wl, uint64_t seed);
 

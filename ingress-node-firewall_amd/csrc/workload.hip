@@ -376,6 +376,19 @@ void infw_wl_destroy(infw_wl *w) {
     delete w;
 }
 
+void infw_wl_uniform_sources(infw_wl *w) {
+    if (w->d_cdf) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(w->dev);
+        (void)hipFree(w->d_cdf);
+        (void)hipSetDevice(prev);
+        w->d_cdf = nullptr;
+    }
+    w->cdf.clear();
+    w->params.zipf_cdf = nullptr;
+}
+
 uint64_t infw_wl_n_entries(const infw_wl *w) { return w->keys.size(); }
 const lpm_ip_key_st *infw_wl_keys(const infw_wl *w) { return w->keys.data(); }
 const uint32_t *infw_wl_val_index(const infw_wl *w) { return w->val_index.data(); }

@@ -252,6 +252,7 @@ _wsig = {
     "infw_wl_templates": (C.c_void_p, [C.c_void_p]),
     "infw_wl_params": (P(GenParams), [C.c_void_p]),
     "infw_wl_set_packet_seed": (None, [C.c_void_p, C.c_uint64]),
+    "infw_wl_uniform_sources": (None, [C.c_void_p]),
     "infw_wl_frames": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_int]),
     "infw_wl_tuples": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]),

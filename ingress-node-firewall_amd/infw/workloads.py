@@ -75,6 +75,10 @@ class Workload:
     def params(self) -> N.GenParams:
         return N.wl.infw_wl_params(self._h).contents
 
+    def uniform_sources(self) -> None:
+        """Draw sources uniformly over the prefixes (no Zipf head); tables unchanged."""
+        N.wl.infw_wl_uniform_sources(self._h)
+
     def set_packet_seed(self, seed: int) -> None:
         N.wl.infw_wl_set_packet_seed(self._h, seed)
 

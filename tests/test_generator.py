@@ -33,3 +33,13 @@ def test_workload_mix_is_as_specified():
     assert 0.55 < (proto == 6).mean() < 0.65
     assert ((t[:, 6] >> 24) < 54).mean() > 0.001        # some truncated frames
     assert (t[:, 5] >= 54).mean() > 0.99                  # frame lengths U[54, 1514]
+
+
+def test_uniform_sources_flattens_the_head():
+    """bench.py --uniform: sources uniform over the prefixes (no Zipf head), tables unchanged."""
+    z = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    u = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    u.uniform_sources()
+    assert np.array_equal(z.keys_bytes(), u.keys_bytes())
+    top = lambda wl: np.sort(np.unique(wl.tuples(0, 50000)[:, 0], return_counts=True)[1])[-2]  # [-1]: word 0 of non-IP
+    assert top(z) > 20 * top(u)
