@@ -74,6 +74,8 @@ struct Variant {
     int cuckoo = 0;   // 1: IPv6 groups in the two-choice table above (absent groups touch both buckets)
     int mini = 0;     // > 0: 16-B mini entry per (list, class, part) holding <= mini segments; others add the 64-B line
     int pairing = 0;  // 1: compiled parts, entry line at ((list * 16 + part) * 8 + cls) * 64 (classes of one part adjacent)
+    int adapt = 0;    // 1: per-(list, class) part count — the fewest of 1..16 parts of <= 20 segments each — inside
+                      // the compiled 16-line region (lines past the count are never touched)
 };
 
 }  // namespace
@@ -130,7 +132,8 @@ int main(int argc, char **argv) {
                             {"stride128", false, false, 0, 64, 128}, {"cls_paired", false, false, 0, 64, 64, 0, 0, 1},
                             {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1},
                             {"list_minor", false, false, 0, 64, 64, 0, 0, 0, 2},
-                            {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3}};
+                            {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3},
+                            {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1}};
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -391,6 +394,29 @@ int main(int argc, char **argv) {
                     tc[nt - 1].addr = 3 * kSpace + (((uint64_t)(l1 - 1) * 16 + (val >> 12)) * 8 + cls) * 64;
                 if (t.dt_plog2 && V.pairing == 2)  // list-minor: (class, part) major, adjacent lists share a line
                     tc[nt - 1].addr = 3 * kSpace + (((uint64_t)cls * 16 + (val >> 12)) * h.n_lists + (l1 - 1)) * 64;
+                if (t.dt_plog2 == 4 && V.adapt) {  // fewest parts (1 << p) whose every part holds <= 20 segments
+                    static std::vector<int8_t> pbest;
+                    if (pbest.empty()) pbest.assign((size_t)h.n_lists * INFW_NCLS, -1);
+                    int8_t &pb = pbest[ei];
+                    if (pb < 0) {
+                        const auto &st = seg_starts[ei];
+                        pb = 4;
+                        for (int pp = 0; pp < 4; pp++) {
+                            const uint32_t w = 65536u >> pp;
+                            bool ok = true;
+                            for (uint32_t q = 0; q < (1u << pp) && ok; q++) {
+                                uint32_t nseg = 1;
+                                for (uint32_t x : st) nseg += x > q * w && x < (q + 1) * w;
+                                ok = nseg <= INFW_DT_CLEAF_SEGS;
+                            }
+                            if (ok) {
+                                pb = (int8_t)pp;
+                                break;
+                            }
+                        }
+                    }
+                    if (pb < 4) tc[nt - 1].addr = 3 * kSpace + (ei * 16 + (val >> (16 - pb))) * 64;
+                }
                 if (t.dt_plog2 && V.mini) {  // mini entry first; the 64-B line only for parts with more segments
                     const auto &st = seg_starts[ei];
                     const uint32_t q = val >> 12, lo = q << 12, hi = lo + 4096;
