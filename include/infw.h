@@ -205,9 +205,11 @@ int infw_num_devices(const infw_ctx *ctx);
 /* LPM-trie map semantics; infw_table_commit publishes it to the GPUs.       */
 /* ------------------------------------------------------------------------ */
 /* Map.Update(key, val, flags)   loader.go:203  (addOrUpdateRules)           */
-/*   -EINVAL prefixLen>160, prefixLen<32 (never produced by BuildEBPFKey,    */
-/*           loader.go:543; the GPU tables key on the exact ifindex),         */
-/*           flags>BPF_EXIST;  -EEXIST / -ENOENT per NOEXIST / EXIST;         */
+/*   -EINVAL prefixLen>160, flags>BPF_EXIST; -EEXIST / -ENOENT per NOEXIST  */
+/*           / EXIST.  prefixLen<32 (a partial ifindex, never produced by     */
+/*           BuildEBPFKey, loader.go:543) is accepted like lpm_trie does: it  */
+/*           covers every ifindex whose key bytes start with its bits, below  */
+/*           the interface's own entries (commits with one are full compiles) */
 /*   -ENOSPC when a new key would exceed max_entries.                        */
 int infw_table_update(infw_ctx *ctx, const struct lpm_ip_key_st *key,
                       const struct rulesVal_st *val, uint64_t flags);

@@ -253,6 +253,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.dte = static_cast<const infw_dt_line *>(e.buf[TB_DTE]);
     t.dtl = static_cast<const infw_dt_line *>(e.buf[TB_DTL]);
     t.levels = static_cast<const uint8_t *>(e.buf[TB_LEVELS]);
+    t.wild = static_cast<const uint32_t *>(e.buf[TB_WILD]);
+    t.n_wild = h.n_wild;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;

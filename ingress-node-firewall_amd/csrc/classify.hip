@@ -485,6 +485,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     if (!lng) sh = short_lookup_cached<kCache, kC24Log>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 }
+                // an ifindex without entries of its own: prefixes shorter than the ifindex (prefixLen < 32)
+                if (slot < 0 && T.n_wild) l1 = infw_wild_match(T.wild, T.n_wild, ifx);
             }
             if (G == 0) lst = l1;
             else if (l1) d = T.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];

@@ -104,6 +104,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     const size_t n_edits = m.dirty.size();
     if (n_edits == 0) return 0;
     if (n_edits > std::max<size_t>(65536, m.nodes.size() / 4)) return full("too many edits");
+    // a partial-ifindex prefix (prefixLen < 32) sets slot defaults under every word of the short table
+    if (h.n_wild) return full("partial-ifindex prefixes present");
 
     // ---- pass 1: classify the edits and check that the layout survives them
     std::vector<Edit> edits;
@@ -117,6 +119,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         e.now = it == m.nodes.end() ? nullptr : &it->second;
         e.was = kv.second;
         if (!e.now && e.was == PendingMap::kAbsent) continue;  // added and removed again
+        if (kv.first.plen < 32) return full("partial-ifindex prefix edited");
         const uint32_t ifx = rd_le32(kv.first.md);
         auto s = inc.slot_of.find(ifx);
         if (s == inc.slot_of.end()) return full("new ifindex");

@@ -99,6 +99,8 @@ struct HostTables {
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;
     uint64_t n_buckets = 0, n_overflow_groups = 0;
+    std::vector<uint32_t> wild{0u, 0u, 0u};  // prefixLen < 32 entries: {plen, key bits, list+1}, longest first
+    uint32_t n_wild = 0;
     std::vector<uint8_t> levels;
     std::vector<uint64_t> desc;
     std::vector<uint64_t> rules;
@@ -128,7 +130,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1
 // The device-resident buffers of one image, in upload order.
 enum TableBuf {
     TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
-    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_COUNT
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_COUNT
 };
 // Host bytes of buffer b (at least one element, like the upload).
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);

@@ -151,6 +151,8 @@ struct infw_dev_tables {
     const uint8_t *levels;     // n_levels distinct long lengths, ascending
     uint32_t n_levels;
     uint32_t dt_plog2;         // decision-table parts per (list, class): 1 << dt_plog2 (0 or 4)
+    const uint32_t *wild;      // entries with prefixLen < 32 (a partial ifindex): {plen, key bits, list+1} x n_wild,
+    uint32_t n_wild;           // longest first; consulted for ifindexes without a slot (their own entries)
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -465,11 +467,22 @@ INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
     return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }
 
+// Longest entry shorter than the ifindex (prefixLen < 32) covering this ifindex: its first plen key bits are
+// the ifindex's little-endian bytes read most significant bit first.  list+1 or 0.
+INFW_TD uint32_t infw_wild_match(const uint32_t *w, uint32_t n, uint32_t ifindex) {
+    const uint32_t k = infw_bswap32(ifindex);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t plen = w[3 * i], m = plen ? ~0u << (32 - plen) : 0u;
+        if (((k ^ w[3 * i + 1]) & m) == 0) return w[3 * i + 2];
+    }
+    return 0;
+}
+
 // list+1 of the longest matching entry, 0 if none.
 template <class T>
 INFW_TD uint32_t infw_lpm(const T &t, int pk, uint32_t ifindex, const uint32_t sa[4]) {
     int slot = infw_if_slot(t, ifindex);
-    if (slot < 0) return 0;
+    if (slot < 0) return infw_wild_match(t.wild, t.n_wild, ifindex);
     uint32_t a32 = infw_bswap32(sa[0]);
     if (pk == INFW_PK_V6 && t.n_levels) {
         uint32_t r = infw_v6_long(t, (uint32_t)slot, a32, sa);

@@ -110,12 +110,6 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
         set_error("update: prefixLen > 160");
         return -EINVAL;
     }
-    if (key->prefixLen < 32) {
-        // An entry shorter than the ifindex would match a set of interfaces;
-        // BuildEBPFKey never produces one (loader.go:543).
-        set_error("update: prefixLen < 32 (partial ifindex prefix) is not supported");
-        return -EINVAL;
-    }
     NodeKey k = make_node(key);
     auto it = nodes.find(k);
     if (it != nodes.end()) {
@@ -558,6 +552,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     {
         std::unordered_map<uint32_t, int> seen;
         for (const auto &kv : m.nodes) {
+            if (kv.first.plen < 32) continue;  // a partial-ifindex prefix names no interface (below)
             uint32_t ifx = rd_le32(kv.first.md);
             if (seen.emplace(ifx, 0).second) ifs.push_back(ifx);
         }
@@ -683,8 +678,37 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     };
     std::vector<LongReal> longs;
     shorts.reserve(m.nodes.size());
+    // Entries shorter than the ifindex (prefixLen < 32: its first bits, in key byte order — the ifindex's
+    // little-endian bytes — BuildEBPFKey never writes one, loader.go:543) cover every interface whose ifindex
+    // bytes start that way, with any address, below every entry of the interface itself.  The longest one
+    // covering an interface with entries becomes that slot's default answer (the short table's words start
+    // from it instead of 0); an ifindex with no entries of its own takes the list of partial prefixes
+    // (infw_wild_lookup), longest first.
+    out.wild.clear();
+    for (const auto &kv : m.nodes)
+        if (kv.first.plen < 32) {
+            const uint8_t *d = kv.first.md;  // masked to plen bits
+            const uint32_t key = (uint32_t)d[0] << 24 | (uint32_t)d[1] << 16 | (uint32_t)d[2] << 8 | d[3];
+            out.wild.push_back(kv.first.plen);
+            out.wild.push_back(key);
+            out.wild.push_back(list_of_vid[kv.second.vid] + 1);
+        }
+    {
+        std::vector<std::array<uint32_t, 3>> w;
+        for (size_t i = 0; i < out.wild.size(); i += 3) w.push_back({out.wild[i], out.wild[i + 1], out.wild[i + 2]});
+        std::sort(w.begin(), w.end(), [](const std::array<uint32_t, 3> &a, const std::array<uint32_t, 3> &b) {
+            return a[0] != b[0] ? a[0] > b[0] : a[1] < b[1];
+        });
+        out.wild.clear();
+        for (const auto &e : w) out.wild.insert(out.wild.end(), e.begin(), e.end());
+    }
+    out.n_wild = (uint32_t)(out.wild.size() / 3);
+    if (out.wild.empty()) out.wild.assign(3, 0u);  // never an empty device buffer
+    std::vector<uint32_t> slot_default(out.n_slots, 0);
+    for (uint32_t sl = 0; sl < out.n_slots; sl++) slot_default[sl] = infw_wild_match(out.wild.data(), out.n_wild, ifs[sl]);
     for (const auto &kv : m.nodes) {
         const NodeKey &k = kv.first;
+        if (k.plen < 32) continue;
         uint32_t slot = slot_of[rd_le32(k.md)];
         uint32_t P = k.plen - 32;
         uint32_t list1 = list_of_vid[kv.second.vid] + 1;
@@ -742,8 +766,8 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         for (uint32_t slot = 0; slot < out.n_slots; slot++) {
             size_t sj = si;
             while (sj < shorts.size() && shorts[sj].slot == slot) sj++;
-            if (sj == si) continue;
-            t24.assign((size_t)1 << 24, 0u);
+            if (sj == si && !slot_default[slot]) continue;
+            t24.assign((size_t)1 << 24, slot_default[slot]);
             t8.clear();
             for (size_t x = si; x < sj; x++) {
                 const ShortEnt &e = shorts[x];
@@ -964,6 +988,7 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
     case TB_DTE: INFW_HB(dte);
     case TB_DTL: INFW_HB(dtl);
     case TB_LEVELS: INFW_HB(levels);
+    case TB_WILD: INFW_HB(wild);
     default:
         *p = nullptr;
         *bytes = 0;
@@ -974,6 +999,8 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
 infw_dev_tables HostTables::view() const {
     infw_dev_tables t;
     memset(&t, 0, sizeof(t));
+    t.wild = wild.data();
+    t.n_wild = n_wild;
     t.if_keys = if_keys.data();
     t.if_slot = if_slot.data();
     t.if_mask = (uint32_t)if_keys.size() - 1;

@@ -84,7 +84,8 @@ def test_update_flags_and_errors_match_oracle():
 
 def random_key(rng):
     ifx = rng.choice([1, 2, 0xFFFFFFFF])
-    plen = rng.choice([32, 33, 40, 48, 56, 63, 64, 65, 80, 96, 128, 150, 159, 160])
+    # prefixLen < 32: partial-ifindex prefixes (never written by BuildEBPFKey, accepted by the LPM trie)
+    plen = rng.choice([0, 8, 16, 31, 32, 33, 40, 48, 56, 63, 64, 65, 80, 96, 128, 150, 159, 160])
     ip = bytes(rng.getrandbits(8) for _ in range(16))
     if rng.random() < 0.5:  # nested / shared prefixes
         ip = bytes([10, 20]) + ip[2:]
@@ -107,7 +108,7 @@ def test_random_map_ops_match_oracle():
         elif op < 0.7:
             assert c.delete_rc(K(k)) == m.delete(k)
         else:  # LPM lookup with an arbitrary prefixLen
-            q = k[:4] if rng.random() < 0.5 else struct.pack("<I", rng.choice([32, 64, 100, 160]))
+            q = k[:4] if rng.random() < 0.5 else struct.pack("<I", rng.choice([8, 32, 64, 100, 160]))
             q = q + k[4:]
             got = c.lookup(K(q))
             want = m.lookup(q)
@@ -128,6 +129,11 @@ def test_commit_epoch_counts():
     assert c.info()["epoch"] == e0 + 2 and c.info()["n_entries"] == 1
 
 
-def test_prefix_shorter_than_ifindex_rejected():
+def test_prefix_shorter_than_ifindex_accepted():
+    """lpm_trie accepts prefixLen < 32 (a partial ifindex); so does the map — matching is tests/test_golden.py's."""
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
-    assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(key(24, 1, b"")), infw.RulesValSt()) == -22
+    m = orc.OracleMap()
+    k = key(24, 1, b"")
+    assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt()) == m.update(k, bytes(1200)) == 0
+    assert bytes(c.lookup(infw.LpmIpKeySt.from_buffer_copy(key(64, 1, b"\x0a\0\0\x01")))) == bytes(1200)
+    c.commit()

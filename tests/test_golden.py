@@ -134,6 +134,65 @@ def test_loader_partial_failure_publishes_applied_updates():
     assert list(ver) == [1, 1, 2]  # the two applied keys are in the published epoch (XDP_DROP), the third is not
 
 
+def partial_ifindex_case():
+    """A table with keys shorter than the ifindex and packets from interfaces with and without entries of their own:
+    (entries [(key bytes, rule id)], values {rule id: 1200 B}, hdr, cap, pl, ifindex array, tuples)."""
+    import struct
+    rng = np.random.default_rng(3)
+    entries = [(goenc.build_key(1, "10.0.0.0/8"), 3), (goenc.build_key(0x102, "10.1.0.0/16"), 4),
+               (goenc.build_key(0x102, "2001:db8::/32"), 5), (goenc.build_key(0x102, "2001:db8:1::/48"), 6),
+               (goenc.build_key(2, "0.0.0.0/0"), 7),
+               (struct.pack("<II", 0, 0) + bytes(16), 8),                              # every ifindex
+               (struct.pack("<II", 8, 0x02) + bytes(16), 9),                           # low byte 0x02
+               (struct.pack("<II", 16, 0x0102) + bytes(16), 10),                       # low bytes 02 01
+               (struct.pack("<II", 31, 0x00000702) + bytes(16), 11)]
+    vals = {rid: goenc.raw_value([{"slot": 1, "ruleId": rid, "protocol": 0, "dstPortStart": 0, "dstPortEnd": 0,
+                                   "icmpType": 0, "icmpCode": 0, "action": 1 + rid % 2}]) for _, rid in entries}
+    ifxs = [1, 2, 3, 0x102, 0x202, 0x10102, 0x702, 0x703, 0x8702, 7]
+    frames, fifx = [], []
+    for k in range(3000):
+        src = rng.choice(["10.%d.%d.%d" % tuple(rng.integers(0, 256, 3)), "11.1.2.3",
+                          "2001:db8:%x::%x" % (rng.integers(0, 3), rng.integers(0, 999)), "2002::1"])
+        frames.append(frame(src, proto="tcp", dport=80))
+        fifx.append(ifxs[k % len(ifxs)])
+    hdr, cap, pl = snapshots(frames)
+    fifx = fifx
+    return entries, vals, hdr, cap, pl, fifx, W.pack_frames(hdr, cap, pl, fifx)
+
+
+def test_partial_ifindex_prefixes():
+    """Keys shorter than the ifindex (prefixLen < 32; lpm_trie accepts them, BuildEBPFKey never writes one): they
+    match every interface whose ifindex bytes (little-endian, as in the key) start with their bits, below every
+    entry of the interface itself — including interfaces with no entries at all.  Compiled host tables vs the
+    oracle, in both short-table forms, and a later full commit without them.  On the GPU:
+    test_gpu_parity.py::test_partial_ifindex_prefixes_on_device."""
+    entries, vals, hdr, cap, pl, fifx, tup = partial_ifindex_case()
+    for mode in ("dir24", "compressed"):
+        import os
+        os.environ["INFW_SHORT_TABLE"] = mode
+        try:
+            c = infw.Classifier(flags=infw.F_HOST_ONLY)
+            m = orc.OracleMap()
+            for kb, rid in entries:
+                assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid])) == 0
+                assert m.update(kb, vals[rid]) == 0
+            c.commit()
+            want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
+            got = c.debug_walk(tup)
+            assert np.array_equal(got, want), mode
+            assert len({int(r) >> 8 for r in want}) >= 6  # defaults, own entries and unknown ifindexes all seen
+            assert [bytes(k) for k, _ in c.iterate()] == list(m.keys())
+            # delete the partial prefixes: the next commit (full) drops the defaults
+            for kb, rid in entries[5:]:
+                assert c.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb)) == m.delete(kb) == 0
+            c.commit()
+            assert c.info()["commit_mode"] == infw.COMMIT_FULL
+            want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
+            assert np.array_equal(c.debug_walk(tup), want), mode
+        finally:
+            del os.environ["INFW_SHORT_TABLE"]
+
+
 def test_ebpfsyncer_key_sets():
     """TestVerifyBPFKeysAfterInterfaceIngressRulesUpdate: the map's key set after each sync."""
     doc = load("ref_ebpfsyncer_keys.json")

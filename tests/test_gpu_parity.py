@@ -276,6 +276,31 @@ def test_event_samples():
                 assert E.drain(got, k, names)[1][0] == f"Perf event ring buffer full, dropped {k - 16} samples"
 
 
+def test_partial_ifindex_prefixes_on_device():
+    """Keys shorter than the ifindex (prefixLen < 32) through the kernel: slot defaults baked into the short table
+    (both forms) and the partial-prefix list for interfaces without entries, vs the oracle."""
+    import os
+    import orc
+    from test_golden import partial_ifindex_case
+    entries, vals, hdr, cap, pl, fifx, tup = partial_ifindex_case()
+    dev = torch.device("cuda", 0)
+    for mode in ("dir24", "compressed"):
+        os.environ["INFW_SHORT_TABLE"] = mode
+        try:
+            c = infw.Classifier(devices=[0])
+            m = orc.OracleMap()
+            for kb, rid in entries:
+                c.update(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid]))
+                m.update(kb, vals[rid])
+            c.commit()
+        finally:
+            del os.environ["INFW_SHORT_TABLE"]
+        gres, gver = gpu_run(c, SoaBatch.from_tuples(tup, dev), tup.shape[0])
+        want, over, ost, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
+        assert np.array_equal(gres, want), mode
+        assert np.array_equal(gver, over) and np.array_equal(c.stats_read_all(), ost), mode
+
+
 def test_device_frame_generator():
     """The bench's frames-in-HBM input (bench.py --from-frames): the device frame generator writes the host frame
     builder's header snapshots at the stride, and pack -> classify of them equals the oracle on those frames."""
