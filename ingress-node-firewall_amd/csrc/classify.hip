@@ -93,24 +93,41 @@ __device__ __forceinline__ uint32_t scan_tail(const uint64_t *__restrict__ rules
 // First-match result from the decision-table lines of (list, cls) (infw_tables.h),
 // one lane per packet: the entry line, and for S > 10 one leaf line, each read
 // whole (four 16-B loads of one 64-B line, issued back to back).
-__device__ __forceinline__ uint32_t lt2(uint32_t w, uint32_t v) { return infw_count_lt(w, v); }
+// Keys below v in u16 pairs, two at a time in packed 16-bit math: v - key saturates to 0 unless key < v,
+// min(., 1) makes it an indicator, and the two halves accumulate separately (1.5 VALU per key instead of
+// a compare, a select and an add-with-carry per key).
+struct KeyCount {
+    uint32_t vv, acc = 0;
+    __device__ __forceinline__ explicit KeyCount(uint32_t v) : vv(v | v << 16) {}
+    __device__ __forceinline__ void add(uint32_t w) {
+        // per half: sat(v - key) > 0 <=> key < v; min(., 1) -> 0/1.  The halves count at most 15 each, so
+        // the indicators accumulate in one 32-bit add without a carry crossing between them.
+        uint32_t d, r;
+        asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(vv), "v"(w));
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(d), "s"(0x00010001u));
+        acc += r;
+    }
+    __device__ __forceinline__ uint32_t total() const { return (acc & 0xFFFFu) + (acc >> 16); }
+};
 __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
                                               uint32_t list, int cls, uint32_t v, uint32_t plog2) {
     const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + infw_dt_slot(list, cls, v, plog2));
     u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
     if (a[0] & INFW_DT_ROOT) {
-        const uint32_t g = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
-                           lt2(b[3], v) + lt2(c[0], v) + lt2(c[1], v) + lt2(c[2], v) + lt2(c[3], v) + lt2(d[0], v) +
-                           lt2(d[1], v) + lt2(d[2], v) + lt2(d[3], v);
-        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g));
+        KeyCount g(v);
+        g.add(a[1]); g.add(a[2]); g.add(a[3]); g.add(b[0]); g.add(b[1]); g.add(b[2]); g.add(b[3]);
+        g.add(c[0]); g.add(c[1]); g.add(c[2]); g.add(c[3]); g.add(d[0]); g.add(d[1]); g.add(d[2]); g.add(d[3]);
+        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g.total()));
         a = l[0];
         b = l[1];
         c = l[2];
         d = l[3];
     }
     if (a[0] & INFW_DT_COMPACT) {  // 19 u16 keys in w[1..10], u8 result codes in w[11..15]
-        const uint32_t k = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v) + lt2(b[2], v) +
-                           lt2(b[3], v) + lt2(c[0], v) + lt2(c[1], v) + lt2(c[2], v);
+        KeyCount kc(v);
+        kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]); kc.add(b[2]); kc.add(b[3]);
+        kc.add(c[0]); kc.add(c[1]); kc.add(c[2]);
+        const uint32_t k = kc.total();
         uint32_t w = c[3];
         w = k >= 4 ? d[0] : w;
         w = k >= 8 ? d[1] : w;
@@ -118,7 +135,9 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
         w = k >= 16 ? d[3] : w;
         return infw_dt_code_result(__builtin_amdgcn_ubfe(w, 8 * (k & 3u), 8));
     }
-    const uint32_t k = lt2(a[1], v) + lt2(a[2], v) + lt2(a[3], v) + lt2(b[0], v) + lt2(b[1], v);
+    KeyCount kc(v);
+    kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]);
+    const uint32_t k = kc.total();
     uint32_t r = b[2];
     r = k >= 1 ? b[3] : r;
     r = k >= 2 ? c[0] : r;

@@ -11,7 +11,7 @@ import os
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(_PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libinfw.so")
+LIB_PATH = os.environ.get("INFW_LIB") or os.path.join(LIB_DIR, "libinfw.so")  # INFW_LIB: A/B builds (tools/)
 WL_LIB_PATH = os.path.join(LIB_DIR, "libinfw_workload.so")
 
 MAX_TARGETS = 1024
