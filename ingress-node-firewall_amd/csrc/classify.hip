@@ -68,6 +68,19 @@ __device__ __forceinline__ uint32_t readlane(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
+// Sum over the 64 lanes of a wave with every lane active (DPP: row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast 15/31 across rows; lane 63 ends with the total).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    uint32_t v = x;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return readlane(v, 63);
+}
+
 __device__ __forceinline__ bool rec_match(uint64_t rec, uint32_t v) {
     const uint32_t lo = (uint32_t)rec & 0xFFFFu, hi = (uint32_t)(rec >> 16) & 0xFFFFu;
     return lo <= v && v <= hi;
@@ -563,8 +576,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 const int s0 = __builtin_amdgcn_readlane(s, lead);
                 const bool mine = s == s0;
                 const uint64_t grp = __ballot(mine);
-                unsigned long long by = mine ? (unsigned long long)plen : 0ull;
-                for (int off = 32; off > 0; off >>= 1) by += __shfl_xor(by, off);
+                // the group's byte count: two 32-bit DPP reductions of the frame lengths' 16-bit halves (a sum of
+                // 64 halves cannot overflow 32 bits), not a 64-bit butterfly of 12 ds_bpermute (every lane active)
+                const uint32_t b_lo = mine ? plen & 0xFFFFu : 0u, b_hi = mine ? plen >> 16 : 0u;
+                const unsigned long long by = (unsigned long long)wave_sum(b_lo) + ((unsigned long long)wave_sum(b_hi) << 16);
                 if (lane == lead) {
                     atomicAdd(&s_pk[s0], (uint32_t)__popcll(grp));
                     atomicAdd(&s_by[s0], by);
