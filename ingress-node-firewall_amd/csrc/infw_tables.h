@@ -218,29 +218,30 @@ INFW_TD void infw_mask128(uint32_t len, uint64_t *hi, uint64_t *lo) {
 // Parse result of one tuple (ingress_node_firewall_main + ip_extract_l4info).
 enum { INFW_PK_DROP_SHORT = 0, INFW_PK_PASS_NONIP = 1, INFW_PK_UNDEF = 2, INFW_PK_V4 = 3, INFW_PK_V6 = 4 };
 
+// Written as bitwise ops and selects, not a switch or short-circuit tests: on the GPU every lane of a wave
+// then takes the same path (a switch over the protocol compiles into a tree of divergent branches and
+// exec-mask bookkeeping, ~120 instructions per wave).  *cls and *val are set on every path; they mean
+// something only when V4 / V6 is returned.
 INFW_TD int infw_parse(uint32_t meta, uint32_t l4word, int *cls, uint32_t *val) {
-    uint32_t et = meta & 0xFFFFu, proto = (meta >> 16) & 0xFFu, cap = meta >> 24;
-    if (cap < 14) return INFW_PK_DROP_SHORT;                      // kernel.c:423-426
-    int v4;
-    if (et == 0x0800) v4 = 1;                                     // :428
-    else if (et == 0x86DD) v4 = 0;                                // :432
-    else return INFW_PK_PASS_NONIP;                               // :436-438
-    uint32_t l4 = v4 ? 34u : 54u;                                 // :104, :111
-    uint32_t need;
-    int c;
-    switch (proto) {                                              // :117-172
-    case 6: need = 20; c = INFW_CLS_TCP; break;
-    case 17: need = 8; c = INFW_CLS_UDP; break;
-    case 132: need = 12; c = INFW_CLS_SCTP; break;
-    case 1: need = 8; c = v4 ? INFW_CLS_ICMP4 : INFW_CLS_1_ON_V6; break;
-    case 58: need = 8; c = v4 ? INFW_CLS_58_ON_V4 : INFW_CLS_ICMP6; break;
-    default: return INFW_PK_UNDEF;
-    }
-    if (cap < l4 + need) return INFW_PK_UNDEF;                    // truncated header
-    if (c <= INFW_CLS_SCTP) *val = (l4word >> 8 & 0xFF00u) | (l4word >> 24);  // ntohs(dest)
-    else *val = (l4word << 8 & 0xFF00u) | (l4word >> 8 & 0xFFu);              // type << 8 | code
-    *cls = c;
-    return v4 ? INFW_PK_V4 : INFW_PK_V6;
+    const uint32_t et = meta & 0xFFFFu, proto = (meta >> 16) & 0xFFu, cap = meta >> 24;
+    const uint32_t v4 = et == 0x0800, v6 = et == 0x86DD;                 // kernel.c:428, :432
+    const uint32_t tcp = proto == 6, udp = proto == 17, sctp = proto == 132, ic1 = proto == 1, ic58 = proto == 58;
+    const uint32_t known = tcp | udp | sctp | ic1 | ic58;                // :117-172, else UNDEF
+    // fixed L4 offset 34 / 54 (:104, :111) plus the header the protocol's case reads: tcphdr 20, sctphdr 12,
+    // udphdr / icmphdr / icmp6hdr 8 — a truncated header is UNDEF
+    const uint32_t need = (v4 ? 34u : 54u) + 8u + tcp * 12u + sctp * 4u;
+    // class: TCP 0, UDP 1, SCTP 2, proto 1 -> ICMP4 (3) on IPv4 / 1_ON_V6 (6), proto 58 -> 58_ON_V4 (5) / ICMP6 (4)
+    const uint32_t c = udp * (uint32_t)INFW_CLS_UDP + sctp * (uint32_t)INFW_CLS_SCTP +
+                       ic1 * (v4 ? (uint32_t)INFW_CLS_ICMP4 : (uint32_t)INFW_CLS_1_ON_V6) +
+                       ic58 * (v4 ? (uint32_t)INFW_CLS_58_ON_V4 : (uint32_t)INFW_CLS_ICMP6);
+    const uint32_t port = (l4word >> 8 & 0xFF00u) | (l4word >> 24);         // ntohs(dest)
+    const uint32_t tc = (l4word << 8 & 0xFF00u) | (l4word >> 8 & 0xFFu);    // type << 8 | code
+    *val = c <= (uint32_t)INFW_CLS_SCTP ? port : tc;
+    *cls = (int)c;
+    int pk = v4 ? INFW_PK_V4 : INFW_PK_V6;
+    pk = (known & (uint32_t)(cap >= need)) ? pk : INFW_PK_UNDEF;
+    pk = (v4 | v6) ? pk : INFW_PK_PASS_NONIP;                           // :436-438
+    return cap < 14 ? INFW_PK_DROP_SHORT : pk;                          // :423-426
 }
 
 INFW_TD uint32_t infw_count_lt(uint32_t w, uint32_t v) {  // keys (two u16) below v
