@@ -42,9 +42,11 @@ constexpr uint32_t kB6C0 = 0x00000001u, kB6C1 = 0x5bd1e995u, kB6C2 = 0x9e3779b9u
 // plain words are cached; inline /24s and tbl8 groups take the table path.
 // Decode a DIR-24-8 word for address a32 (tbl8 only for a /24 with > 3 runs).
 __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t w, uint32_t a32) {
-    if (!(w & INFW_D24_GROUP)) return (uint32_t)w;
-    if (w & INFW_D24_INLINE) return infw_d24_inline(w, a32 & 0xFFu);
-    return T.tbl8[((uint64_t)(uint32_t)w << 8) | (a32 & 0xFFu)];
+    // plain and inline words decode as selects; only a tbl8 group (a /24 of > 3 runs) branches to its load
+    const uint32_t inl = infw_d24_inline(w, a32 & 0xFFu);
+    uint32_t v = (w & INFW_D24_GROUP) ? inl : (uint32_t)w;
+    if ((w & (INFW_D24_GROUP | INFW_D24_INLINE)) == INFW_D24_GROUP) v = T.tbl8[((uint64_t)(uint32_t)w << 8) | (a32 & 0xFFu)];
+    return v;
 }
 
 template <bool kCache, int kLog>
