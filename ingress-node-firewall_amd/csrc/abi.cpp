@@ -256,6 +256,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.wild = static_cast<const uint32_t *>(e.buf[TB_WILD]);
     t.n_wild = h.n_wild;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
+    t.if_mult = h.if_mult;
+    t.if_shift = h.if_shift;
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;
     t.bmask = h.btab.size() - 1;

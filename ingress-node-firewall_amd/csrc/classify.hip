@@ -437,7 +437,11 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             if (!(kAblate & 1)) {
                 // ifindex -> slot (LDS copy of the open-addressed map)
                 int slot;
-                if (if_in_lds) {
+                if (if_in_lds && T.if_mult) {  // collision-free placement: one probe, no loop
+                    const uint32_t h = (ifx * T.if_mult) >> T.if_shift;
+                    const uint32_t k = s_ifk[h], sl = s_ifs[h];
+                    slot = k == ifx && sl != INFW_IF_EMPTY ? (int)sl : -1;
+                } else if (if_in_lds) {
                     uint32_t h = infw_if_hash(ifx) & T.if_mask;
                     for (;;) {
                         const uint32_t sl = s_ifs[h];

@@ -86,6 +86,7 @@ void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes);
 // ------------------------------------------------------------------------
 struct HostTables {
     std::vector<uint32_t> if_keys, if_slot;
+    uint32_t if_mult = 0, if_shift = 0;  // collision-free placement (0: open addressing)
     uint32_t n_slots = 0;
     std::vector<uint32_t> l16;    // n_slots << 16
     std::vector<infw_bnode> nodes;

@@ -134,6 +134,7 @@ struct infw_dev_tables {
     const uint32_t *if_slot;   // INFW_IF_EMPTY = free
     uint32_t if_mask;
     uint32_t n_slots;
+    uint32_t if_mult, if_shift;  // != 0: ifindex i sits at (i * if_mult) >> if_shift (no probing)
     const uint32_t *l16;       // n_slots << 16
     const struct infw_bnode *nodes;
     const uint32_t *vpool;
@@ -292,6 +293,10 @@ INFW_TD uint32_t infw_dt_eval(const T &t, uint32_t list, int cls, uint32_t v) {
 // Table pointers are read through T so host and device share the walk.
 template <class T>
 INFW_TD int infw_if_slot(const T &t, uint32_t ifindex) {
+    if (t.if_mult) {
+        const uint32_t h = (ifindex * t.if_mult) >> t.if_shift;
+        return t.if_keys[h] == ifindex && t.if_slot[h] != INFW_IF_EMPTY ? (int)t.if_slot[h] : -1;
+    }
     uint32_t h = infw_if_hash(ifindex) & t.if_mask;
     for (;;) {
         uint32_t s = t.if_slot[h];

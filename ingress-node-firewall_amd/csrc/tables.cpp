@@ -568,11 +568,40 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     {
         uint32_t cap = 16;
         while (cap < 2 * out.n_slots) cap <<= 1;
+        // a collision-free multiplier when one exists for up to 256 entries: ifindex i sits at
+        // (i * if_mult) >> if_shift, so the kernel resolves an ifindex with one LDS probe and no loop
+        // (infw_if_slot); otherwise open addressing from infw_if_hash
+        out.if_mult = 0;
+        out.if_shift = 0;
+        for (uint32_t c = cap; c <= 256 && !out.if_mult; c <<= 1) {
+            int lg = 0;
+            while ((1u << lg) < c) lg++;
+            for (uint32_t k = 0; k < 256 && !out.if_mult; k++) {
+                const uint32_t m = (0x9E3779B1u + k * 0x6A09E668u) | 1u;
+                std::vector<uint8_t> used(c, 0);
+                bool ok = true;
+                for (uint32_t s = 0; s < out.n_slots && ok; s++) {
+                    const uint32_t h = (ifs[s] * m) >> (32 - lg);
+                    ok = !used[h];
+                    used[h] = 1;
+                }
+                if (ok) {
+                    out.if_mult = m;
+                    out.if_shift = 32 - lg;
+                    cap = c;
+                }
+            }
+        }
         out.if_keys.assign(cap, 0);
         out.if_slot.assign(cap, INFW_IF_EMPTY);
         for (uint32_t s = 0; s < out.n_slots; s++) {
-            uint32_t h = infw_if_hash(ifs[s]) & (cap - 1);
-            while (out.if_slot[h] != INFW_IF_EMPTY) h = (h + 1) & (cap - 1);
+            uint32_t h;
+            if (out.if_mult) {
+                h = (ifs[s] * out.if_mult) >> out.if_shift;
+            } else {
+                h = infw_if_hash(ifs[s]) & (cap - 1);
+                while (out.if_slot[h] != INFW_IF_EMPTY) h = (h + 1) & (cap - 1);
+            }
             out.if_keys[h] = ifs[s];
             out.if_slot[h] = s;
         }
@@ -1004,6 +1033,8 @@ infw_dev_tables HostTables::view() const {
     t.if_keys = if_keys.data();
     t.if_slot = if_slot.data();
     t.if_mask = (uint32_t)if_keys.size() - 1;
+    t.if_mult = if_mult;
+    t.if_shift = if_shift;
     t.n_slots = n_slots;
     t.l16 = l16.data();
     t.tbl24 = tbl24.data();
