@@ -49,10 +49,14 @@ __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t
     return v;
 }
 
-template <bool kCache, int kLog>
+// kLean: the epoch has no compressed short table (DIR-24-8 or none), no overflowed IPv6 group and no
+// partial-ifindex prefix (infw_dev_tables.lean), so those paths are compiled out.
+template <bool kCache, int kLog, bool kLean = false>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                         unsigned long long *s_c24) {
-    if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u) return infw_short_lookup(T, slot, a32);
+    if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u)
+        return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(T, slot, a32) : 0u)
+                     : infw_short_lookup(T, slot, a32);
     const uint32_t key = slot << 24 | a32 >> 8;
     const uint32_t idx = (key * 0x9E3779B1u) >> (32 - kLog);
     const unsigned long long e = s_c24[idx];
@@ -172,6 +176,7 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
 // for the header and one per record examined.
 // Finish a first bucket probe whose header h and first record r0 are already loaded:
 // most groups hold one record, so records 1..2 (and further probes) load on demand.
+template <bool kLean = false>
 __device__ __forceinline__ uint32_t v6_finish(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                              const uint32_t sa[4], uint64_t i, u32x4 h, u32x4 r0) {
     const uint32_t mid = infw_bswap32(sa[1]);
@@ -180,7 +185,7 @@ __device__ __forceinline__ uint32_t v6_finish(const infw_dev_tables &T, uint32_t
         if (h[0] == 0) return 0;
         if (h[0] == slot + 1 && h[1] == a32) {
             const uint32_t nb = h[2];
-            if (nb == INFW_BUCKET_OVERFLOW) return infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
+            if (nb == INFW_BUCKET_OVERFLOW) return kLean ? 0u : infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
             if (nb >= 1 && infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
             if (nb >= 2) {
                 const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + i);
@@ -294,7 +299,7 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128)>
+          bool kPrefetch = !(kAblate & 128), bool kLean = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         br0 = b[1];
                     }
                     if (need6) {
-                        lng = v6_finish(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                        lng = v6_finish<kLean>(T, (uint32_t)slot, a32, sw, bi, bh, br0);
                         if (b6ok && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
                             s_b6[2 * b6idx] = u32x4{b6tag ^ kB6C0, br0[0], b6tag ^ kB6C1, br0[1]};
                             s_b6[2 * b6idx + 1] = u32x4{b6tag ^ kB6C2, br0[2], b6tag ^ kB6C3, br0[3]};
@@ -512,9 +517,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
                             s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
                     } else if (!v6 && !d24) {
-                        sh = infw_short_lookup(T, (uint32_t)slot, a32);  // compressed / no short table
+                        sh = kLean ? 0u : infw_short_lookup(T, (uint32_t)slot, a32);  // compressed / no short table
                     }
-                    if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log>(T, (uint32_t)slot, a32, s_c24);
+                    if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log, kLean>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 } else if (slot >= 0) {  // diagnostic 512: the sequential form (bucket round, then tbl24 round)
                     const uint32_t a32 = infw_bswap32(sa.x);
@@ -524,7 +529,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     l1 = lng ? lng : sh;
                 }
                 // an ifindex without entries of its own: prefixes shorter than the ifindex (prefixLen < 32)
-                if (slot < 0 && T.n_wild) l1 = infw_wild_match(T.wild, T.n_wild, ifx);
+                if (!kLean && slot < 0 && T.n_wild) l1 = infw_wild_match(T.wild, T.n_wild, ifx);
             }
             if (G == 0) lst = l1;
             else if (l1) d = T.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
@@ -638,14 +643,15 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0>
+          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log>), dim3(g), dim3(kBlock), 0,
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean>),
+                       dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
 
@@ -662,6 +668,8 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)  // the default shape without the rare paths
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6) launch<768, 0, 0, false, 6, false, kC, 12, 9>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else return false;

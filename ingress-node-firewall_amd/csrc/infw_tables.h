@@ -154,6 +154,8 @@ struct infw_dev_tables {
     uint32_t dt_plog2;         // decision-table parts per (list, class): 1 << dt_plog2 (0 or 4)
     const uint32_t *wild;      // entries with prefixLen < 32 (a partial ifindex): {plen, key bits, list+1} x n_wild,
     uint32_t n_wild;           // longest first; consulted for ifindexes without a slot (their own entries)
+    uint32_t lean;             // 1: no compressed short table, no overflowed IPv6 group, no partial-ifindex prefix —
+                               // the kernel may launch without those code paths (fewer live registers)
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
