@@ -190,10 +190,12 @@ INFW_TD uint64_t infw_b6_key(uint32_t slot, uint32_t top) {
 // Does record r cover address bits 32..127 (mid, lo)?
 INFW_TD bool infw_rec_match(uint32_t rmid, uint64_t rlo, uint32_t meta, uint32_t mid, uint64_t lo) {
     const uint32_t L = (meta >> 25) + 32;  // 33..128
-    // masks as selects (no branch): the first L - 32 bits of mid (all of it from /64 on), then L - 64 bits of lo
-    const uint32_t mmid = L >= 64 ? ~0u : ~0u << ((64 - L) & 31);
-    const uint64_t mlo = L <= 64 ? 0ull : L >= 128 ? ~0ull : ~0ull << ((128 - L) & 63);
-    return (((mid ^ rmid) & mmid) | (uint32_t)(((lo ^ rlo) & mlo) != 0)) == 0;
+    if (L <= 64) {
+        const uint32_t m = ~0u << (64 - L);  // L-32 in 1..32 leading bits of mid
+        return ((mid ^ rmid) & m) == 0;
+    }
+    const uint64_t m = L >= 128 ? ~0ull : ~0ull << (128 - L);
+    return mid == rmid && ((lo ^ rlo) & m) == 0;
 }
 
 INFW_TD uint64_t infw_long_hash(uint32_t tag, uint64_t hi, uint64_t lo) {
