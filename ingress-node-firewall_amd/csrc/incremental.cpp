@@ -57,39 +57,34 @@ void mark(std::vector<DirtyRange> &r, int buf, uint64_t off, uint64_t len) {
     if (len) r.push_back(DirtyRange{(uint32_t)buf, off, len});
 }
 
-// The entry of exactly /L (L <= 32 address bits) at address a on this ifindex, if any.
-inline const NodeVal *exact_short(const PendingMap &m, const uint8_t ifx_le[4], uint32_t a, uint32_t L) {
-    if (!m.len_count[L + 32]) return nullptr;
-    uint8_t md[20];
-    short_md(md, ifx_le, a);
-    NodeKey k;
-    k.plen = L + 32;
-    mask_bits(md, k.plen, k.md, 20);
-    auto it = m.nodes.find(k);
-    return it == m.nodes.end() ? nullptr : &it->second;
-}
-
-// Longest-match answers over the /L block at address a, for every /Lend sub-block: depth-first
-// over the block's sub-prefixes, one probe per populated length and node, starting from v = the
-// answer of the lengths below L.  About two probes per sub-block, where probing every length for
-// every sub-block costs (Lend - L + 1) — a /16 edit re-derives its 256 tbl24 words with ~511
-// probes instead of ~256 x 9.
-template <class Leaf>
-void descend(const PendingMap &m, const uint8_t ifx_le[4], uint32_t a, uint32_t L, uint32_t Lend,
-             const NodeVal *v, Leaf &leaf) {
-    if (const NodeVal *e = exact_short(m, ifx_le, a, L)) v = e;
-    if (L == Lend) {
-        leaf(a, v);
-        return;
+// Answers of the /P block at address a of one ifindex at resolution R (24: tbl24 words, 32: tbl8 entries):
+// every unit starts from `base` (the longest entry of length <= P covering the block) and the entries longer
+// than P inside the block are painted over it in ascending length, so each unit ends with its longest match.
+// The entries come from the map's per-block short-key lists — no probe per unit and length.  ans[u] is the
+// answer of unit u (2^(R - P) units).
+void paint(const PendingMap &m, uint32_t ifx, uint32_t a, uint32_t P, uint32_t R, const NodeVal *base,
+           std::vector<const NodeVal *> &ans, std::vector<PendingMap::ShortRef> &tmp) {
+    ans.assign(1ull << (R - P), base);
+    tmp.clear();
+    for (uint32_t lv = 0; lv < R; lv += 8) {  // the level-lv lists hold lengths (lv, lv + 8]
+        if (lv + 8 <= P) continue;
+        if (lv <= P) {  // one block covers the /P block: keep its entries longer than P inside it
+            if (const auto *v = m.sub_list(lv, ifx, a))
+                for (const auto &r : *v)
+                    if (r.L > P && r.L <= R && (P == 0 || (r.a32 >> (32 - P)) == (a >> (32 - P)))) tmp.push_back(r);
+        } else {        // 2^(lv - P) blocks inside the /P block
+            const uint64_t nb = 1ull << (lv - P);
+            for (uint64_t k = 0; k < nb; k++)
+                if (const auto *v = m.sub_list(lv, ifx, a + (uint32_t)(k << (32 - lv))))
+                    for (const auto &r : *v)
+                        if (r.L <= R) tmp.push_back(r);
+        }
     }
-    // a /8, /16 or /24 block with no entry longer than itself (PendingMap::deeper): every sub-block
-    // answers v — no probes below it
-    if ((L == 8 || L == 16 || L == 24) && !m.has_deeper(L, rd_le32(ifx_le), a)) {
-        for (uint64_t k = 0; k < (1ull << (Lend - L)); k++) leaf(a + (uint32_t)(k << (32 - Lend)), v);
-        return;
+    std::sort(tmp.begin(), tmp.end(), [](const PendingMap::ShortRef &x, const PendingMap::ShortRef &y) { return x.L < y.L; });
+    for (const auto &r : tmp) {
+        const uint64_t off = (uint64_t)(r.a32 - a) >> (32 - R);
+        std::fill(ans.begin() + off, ans.begin() + off + (1ull << (R - r.L)), r.v);
     }
-    descend(m, ifx_le, a, L + 1, Lend, v, leaf);
-    descend(m, ifx_le, a | (1u << (31 - L)), L + 1, Lend, v, leaf);
 }
 
 }  // namespace
@@ -108,6 +103,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     if (h.n_wild) return full("partial-ifindex prefixes present");
 
     // ---- pass 1: classify the edits and check that the layout survives them
+    const auto tpa = std::chrono::steady_clock::now();
     std::vector<Edit> edits;
     edits.reserve(n_edits);
     uint64_t short_words = 0;
@@ -260,34 +256,41 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (e.P <= 32) shorts.push_back(&e);
     std::sort(shorts.begin(), shorts.end(), [](const Edit *a, const Edit *b) { return a->P < b->P; });
     uint8_t md[20];
+    std::vector<const NodeVal *> ans, ans8;
+    std::vector<PendingMap::ShortRef> tmp;
+    uint64_t n_refills = 0, n_words = 0;
     // tbl8 entries [j0, j0 + 2^(32 - P)) of group g under /24 i24: the /P block's answers at /32,
-    // from base = the answer of the lengths below P
-    auto refill_group = [&](const uint8_t *ifx, uint32_t i24, uint32_t g, uint32_t j0, uint32_t P, const NodeVal *base) {
+    // from base = the answer of the lengths <= P
+    auto refill_group = [&](uint32_t ifx, uint32_t i24, uint32_t g, uint32_t j0, uint32_t P, const NodeVal *base) {
         uint32_t *t8 = &h.tbl8[(size_t)g << 8];
-        auto leaf = [&](uint32_t a, const NodeVal *v) { t8[a & 0xFFu] = list1(v); };
-        descend(m, ifx, i24 << 8 | j0, P, 32, base, leaf);
+        n_refills++;
+        paint(m, ifx, i24 << 8 | j0, P, 32, base, ans8, tmp);
+        for (size_t u = 0; u < ans8.size(); u++) t8[j0 + u] = list1(ans8[u]);
         mark(ranges, TB_TBL8, (((uint64_t)g << 8) + j0) * 4, (4ull << (32 - P)));
     };
     for (const Edit *e : shorts) {
-        const uint8_t *ifx = e->key->md;
+        const uint8_t *ifx_le = e->key->md;
+        const uint32_t ifx = rd_le32(ifx_le);
         uint64_t *t24 = &h.tbl24[(size_t)e->slot << 24];
         const uint64_t gkey = (uint64_t)e->slot << 24;
         const uint32_t a = e->P ? e->a32 & (~0u << (32 - e->P)) : 0u;
-        short_md(md, ifx, a);
+        short_md(md, ifx_le, a);
         const NodeVal *below = e->P ? m.longest(md, 32, 32 + e->P - 1) : nullptr;  // lengths < P
+        const NodeVal *atP = e->now ? e->now : below;                                 // lengths <= P
         if (e->P <= 24) {
             const uint32_t i0 = a >> 8, cnt = 1u << (24 - e->P);
-            auto leaf24 = [&](uint32_t a24, const NodeVal *v) {  // v: the longest entry <= /24 of this word
-                const uint32_t i = a24 >> 8;
+            n_words += cnt;
+            paint(m, ifx, a, e->P, 24, atP, ans, tmp);  // the longest entry <= /24 of every word
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint32_t i = i0 + k;
                 auto g = h.tbl8_of.find(gkey | i);
                 if (g != h.tbl8_of.end()) {
-                    refill_group(ifx, i, g->second, 0, 24, v);
+                    refill_group(ifx, i, g->second, 0, 24, ans[k]);
                     t24[i] = infw_d24_encode(&h.tbl8[(size_t)g->second << 8], g->second, h.d24_inline);
                 } else {
-                    t24[i] = list1(v);
+                    t24[i] = list1(ans[k]);
                 }
-            };
-            descend(m, ifx, a, e->P, 24, below, leaf24);
+            }
             mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i0) * 8, (uint64_t)cnt * 8);
         } else {
             const uint32_t i = a >> 8;
@@ -304,20 +307,13 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                 h.tbl8_of[gkey | i] = g;
                 h.n_tbl8_groups++;
             }
-            refill_group(ifx, i, g, a & 0xFFu, e->P, below);
+            refill_group(ifx, i, g, a & 0xFFu, e->P, atP);
             t24[i] = infw_d24_encode(&h.tbl8[(size_t)g << 8], g, h.d24_inline);
             mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 8, 8);
         }
     }
 
     const auto tp2 = std::chrono::steady_clock::now();
-    if (getenv("INFW_PATCH_TRACE")) {
-        uint32_t minP = 99;
-        for (const Edit *e : shorts) minP = std::min(minP, e->P);
-        fprintf(stderr, "[patch] %zu edits: lists %.2f ms (%zu new), shorts %.2f ms (%zu, shortest /%u)\n", edits.size(),
-                std::chrono::duration<double, std::milli>(tp1 - tp0).count(), new_vids.size(),
-                std::chrono::duration<double, std::milli>(tp2 - tp1).count(), shorts.size(), minP);
-    }
     // IPv6 buckets
     std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
     for (const auto &kv : inc.slot_of) ifx_of_slot[kv.second] = kv.first;
@@ -350,6 +346,15 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
     }
     h.n_entries = m.nodes.size();
+    if (getenv("INFW_PATCH_TRACE")) {
+        uint32_t minP = 99;
+        for (const Edit *e : shorts) minP = std::min(minP, e->P);
+        const auto tp3 = std::chrono::steady_clock::now();
+        auto ms = [](auto d) { return std::chrono::duration<double, std::milli>(d).count(); };
+        fprintf(stderr, "[patch] %zu edits: checks %.2f ms, lists %.2f ms (%zu new), shorts %.2f ms (%zu, shortest /%u; %llu tbl24 words, %llu tbl8 refills), "
+                "IPv6 groups %.2f ms (%zu)\n", edits.size(), ms(tp0 - tpa), ms(tp1 - tp0), new_vids.size(), ms(tp2 - tp1),
+                shorts.size(), minP, (unsigned long long)n_words, (unsigned long long)n_refills, ms(tp3 - tp2), groups.size());
+    }
     return 0;
 }
 

@@ -57,18 +57,28 @@ struct PendingMap {
     // key was not in the committed set).  Drives the incremental commit.
     static constexpr int64_t kAbsent = -1;
     std::unordered_map<NodeKey, int64_t, NodeKeyHash> dirty;
-    // Short-key occupancy below /8, /16 and /24 blocks: (level, ifindex, block bits) -> entries with
-    // 32 or fewer address bits longer than the block.  Lets an incremental commit fill a block that holds
-    // nothing deeper without probing it (a /8 edit: 65536 DIR-24-8 words).
-    std::unordered_map<uint64_t, uint32_t> deeper;
-    static uint64_t deeper_key(uint32_t level, uint32_t ifindex, uint32_t a32) {
-        return (uint64_t)(level >> 3) << 62 | (uint64_t)ifindex << 24 | (a32 >> (32 - level));
+    // Short keys (1..32 address bits) listed under their enclosing block: (level, ifindex, the address's top
+    // `level` bits) -> the entries with level < L <= level + 8, for level 0, 8, 16, 24.  An incremental commit
+    // paints the DIR-24-8 words (and tbl8 entries) an edit covers from these lists — base answer, then the
+    // longer entries inside the block in ascending length — instead of probing the map per word and length.
+    // The NodeVal pointers stay valid: unordered_map never moves its elements, and a removed key leaves its list.
+    struct ShortRef {
+        uint32_t a32;       // address bits 0..31, masked to L
+        uint32_t L;
+        const NodeVal *v;
+    };
+    std::unordered_map<uint64_t, std::vector<ShortRef>> sub;
+    static uint64_t sub_key(uint32_t level, uint32_t ifindex, uint32_t a32) {
+        return (uint64_t)(level >> 3) << 62 | (uint64_t)ifindex << 24 | (level ? a32 >> (32 - level) : 0u);
     }
-    void count_deeper(const NodeKey &k, int delta);
-    bool has_deeper(uint32_t level, uint32_t ifindex, uint32_t a32) const {
-        auto it = deeper.find(deeper_key(level, ifindex, a32));
-        return it != deeper.end() && it->second != 0;
+    const std::vector<ShortRef> *sub_list(uint32_t level, uint32_t ifindex, uint32_t a32) const {
+        auto it = sub.find(sub_key(level, ifindex, a32));
+        return it == sub.end() ? nullptr : &it->second;
     }
+    void index_short(const NodeKey &k, const NodeVal *v);  // v == nullptr: remove
+    PendingMap() = default;
+    PendingMap(const PendingMap &) = delete;  // `sub` points into `nodes`
+    PendingMap &operator=(const PendingMap &) = delete;
 
     int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
     int remove(const lpm_ip_key_st *key);

@@ -131,24 +131,33 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
     memcpy(v.data + 4, key->ip_data, 16);
     v.vid = pool.intern(val);
     dirty.emplace(k, kAbsent);
-    nodes.emplace(k, v);
-    count_deeper(k, +1);
+    auto ins = nodes.emplace(k, v).first;
+    index_short(k, &ins->second);
     order.insert(k);
     len_count[k.plen]++;
     generation++;
     return 0;
 }
 
-void PendingMap::count_deeper(const NodeKey &k, int delta) {
-    if (k.plen < 32 || k.plen > 64) return;  // only keys of the short (<= 32 address bits) table
+void PendingMap::index_short(const NodeKey &k, const NodeVal *v) {
+    if (k.plen <= 32 || k.plen > 64) return;  // only keys of the short (<= 32 address bits) table, L >= 1
     const uint32_t L = k.plen - 32, ifx = rd_le32(k.md);
     const uint32_t a32 = (uint32_t)k.md[4] << 24 | (uint32_t)k.md[5] << 16 | (uint32_t)k.md[6] << 8 | k.md[7];
-    for (uint32_t level : {8u, 16u, 24u}) {
-        if (L <= level) break;
-        uint32_t &c = deeper[deeper_key(level, ifx, a32)];
-        c += (uint32_t)delta;
-        if (c == 0) deeper.erase(deeper_key(level, ifx, a32));
+    const uint64_t sk = sub_key((L - 1) & ~7u, ifx, a32);
+    if (v) {
+        sub[sk].push_back(ShortRef{a32, L, v});
+        return;
     }
+    auto it = sub.find(sk);
+    if (it == sub.end()) return;
+    auto &vec = it->second;
+    for (size_t i = 0; i < vec.size(); i++)
+        if (vec[i].L == L && vec[i].a32 == a32) {
+            vec[i] = vec.back();
+            vec.pop_back();
+            break;
+        }
+    if (vec.empty()) sub.erase(it);
 }
 
 int PendingMap::remove(const lpm_ip_key_st *key) {
@@ -157,7 +166,7 @@ int PendingMap::remove(const lpm_ip_key_st *key) {
     auto it = nodes.find(k);
     if (it == nodes.end()) return -ENOENT;
     dirty.emplace(k, (int64_t)it->second.vid);
-    count_deeper(it->first, -1);
+    index_short(it->first, nullptr);
     nodes.erase(it);
     order.erase(k);
     len_count[k.plen]--;
@@ -457,6 +466,10 @@ static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
             lines[pl] += a[pl];
             over[pl] += a[5 + pl];
         }
+    if (getenv("INFW_COMPILE_TRACE"))
+        for (uint32_t pl = 0; pl <= 4; pl++)
+            fprintf(stderr, "[compile] %u parts: %llu (list, class, part) lines, %llu need a root + leaf\n", 1u << pl,
+                    (unsigned long long)lines[pl], (unsigned long long)over[pl]);
     for (uint32_t pl = 0; pl < 4; pl++)
         if (over[pl] * 256 <= lines[pl]) return pl;
     return 4;

@@ -314,6 +314,7 @@ int main(int argc, char **argv) {
     }
     if (getenv("CACHESIM_LDS_ONLY")) return 0;
     const char *only = getenv("CACHESIM_VARIANTS");
+    const int xcd_mode = getenv("CACHESIM_XCD") ? atoi(getenv("CACHESIM_XCD")) : 0;
     for (const Variant &V : vars) {
         if (only && !strstr(only, V.name)) continue;
         std::vector<L2> l2(8, L2(4ull << 20));
@@ -435,7 +436,25 @@ int main(int argc, char **argv) {
             L2 &c = l2[(i / 512) % 8];
             for (int k = 0; k < nt; k++) {
                 req[tc[k].s]++;
-                L2 &ck = phases && (tc[k].s == S_ENTRY || tc[k].s == S_LEAF) ? l2b[(i / 512) % 8] : c;
+                L2 *cp = phases && (tc[k].s == S_ENTRY || tc[k].s == S_LEAF) ? &l2b[(i / 512) % 8] : &c;
+                // CACHESIM_XCD=1: decision lines served by the XCD their list hashes to (packets binned by list
+                // between an LPM phase and a decision phase); 2: every line by the XCD its address hashes to (the
+                // eight L2s as one 32-MiB cache: the bound of any XCD-partitioned design)
+                const bool dec = tc[k].s == S_ENTRY || tc[k].s == S_LEAF;
+                // 3: packets grouped by a hash of their source /24 (IPv4) or /32 (IPv6) and the ifindex, one group
+                // per XCD (an RSS-style queue split of the batch); 4: the same by the full source address
+                if (xcd_mode >= 3) {
+                    const uint32_t *q = &tup[i * 8];
+                    const uint32_t a0 = infw_bswap32(q[0]);
+                    uint64_t hk = xcd_mode == 3 ? (pk == INFW_PK_V4 ? (uint64_t)(a0 >> 8) : (uint64_t)a0 | 1ull << 40)
+                                                : ((uint64_t)q[0] << 32 | q[1]) ^ ((uint64_t)q[2] << 32 | q[3]) * 31;
+                    hk = hk * 0x9E3779B97F4A7C15ull + q[4];
+                    cp = &l2[((hk * 0xD6E8FEB86659FD93ull) >> 61) & 7];
+                } else if ((xcd_mode == 1 && dec) || xcd_mode == 2) {
+                    const uint64_t hk = xcd_mode == 1 ? (uint64_t)l1 : tc[k].addr / 128;
+                    cp = &l2[((hk * 0xD6E8FEB86659FD93ull) >> 61) & 7];
+                }
+                L2 &ck = *cp;
                 if (!ck.access(tc[k].addr)) miss[tc[k].s]++;
             }
         }
