@@ -137,6 +137,9 @@ def parse():
     ap.add_argument("--from-frames", type=int, default=0, metavar="STRIDE",
                     help="packer-fed step: raw frames resident in HBM at this stride (e.g. 128) -> infw_pack_frames_c "
                          "-> infw_classify_c, both timed (implies --layout compact)")
+    ap.add_argument("--fused", action="store_true",
+                    help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
+                         "no SoA batch written or read; checked untimed against the packer path's results")
     return ap.parse_args()
 
 
@@ -213,6 +216,20 @@ def main():
     else:
         algo_bytes = ALGO_BYTES_PER_PKT
     results = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    fused_check = None
+    if args.fused:
+        assert args.from_frames, "--fused needs --from-frames STRIDE"
+        if n:  # untimed: the fused kernel's result words == the packer path's (counters: the digest below)
+            ref = torch.empty_like(results)
+            clf.classify_c(batch_c, results=ref)
+            clf.classify_frames(frames, f_lin[:n], f_ifx[:n], n, results=results, pkt_len=f_len[:n], stride=stride)
+            torch.cuda.synchronize()
+            fused_check = bool(torch.equal(ref, results))
+            assert fused_check, "classify_frames differs from pack_frames_c + classify_c"
+            del ref
+            clf.stats_reset()
+        args.layout = "frames"
+        algo_bytes = 27 + 12 * n6 / n  # frame bytes kernel.c reads (11 B IPv4, 23 B IPv6) + 12 B lengths/ifindex + result
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -222,7 +239,12 @@ def main():
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
-        if args.from_frames:
+        if args.fused:
+            if ev is not None:
+                ev[2].record(stream)
+            clf.classify_frames(frames, f_lin[:n], f_ifx[:n], n, results=results, pkt_len=f_len[:n], stride=stride,
+                                stream=stream)
+        elif args.from_frames:
             clf.pack_frames_c(frames, f_lin[:n], f_ifx[:n], batch_c, pkt_len=f_len[:n], stride=stride, stream=stream)
             if ev is not None:
                 ev[2].record(stream)
@@ -283,7 +305,11 @@ def main():
     block, group, bpc = clf.launch()
     kernel = f"classify_kernel<{block}, {group}> ({bpc} workgroups per CU)" + (
         " (family-compact layout)" if args.layout == "compact" else "")
-    if args.from_frames:
+    if args.fused:
+        kernel = "classify_kernel<768, 0> (2 workgroups per CU) (raw frames: infw_classify_frames)"
+        extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,
+                                      "results_equal_packer_path": fused_check}}
+    elif args.from_frames:
         # packer: the frame bytes kernel.c reads (ethertype, L3 proto, source address, first L4 word: 11 B IPv4 /
         # 23 B IPv6) + linear length, frame length, ifindex (12 B) in; the compact tuple (algo_bytes - 4) out
         s6 = (algo_bytes - 24) / 12
@@ -298,7 +324,7 @@ def main():
     else:
         extra_pipe = {}
     wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_uniform" if args.uniform else "") + (
-        "_frames" if args.from_frames else "")
+        "_frames" if args.from_frames else "") + ("_fused" if args.fused else "")
 
     traffic = None
     traffic_from = None

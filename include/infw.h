@@ -283,6 +283,14 @@ int infw_pack_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *fram
 int infw_pack_frames_c(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
                        const struct infw_batch_soa_c_out *out, void *stream);
 
+/* infw_classify straight from the frames (no SoA batch written or read: the  */
+/* kernel builds infw_pack_header()'s tuple from each frame's bytes [10, 58)  */
+/* in LDS — the XDP program's own input, kernel.c:412-462 per frame).          */
+/* Identical results and counters to infw_pack_frames + infw_classify.        */
+/* Frames must be readable over [frame, frame + min(linear_len, 58)).          */
+int infw_classify_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
+                         uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */
 /*  - Deny events (kernel.c:392-399, ingress_node_firewall_events_map): one  */

@@ -17,6 +17,9 @@
 
 #include "infw_internal.h"
 
+extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_frame_batch *fb, uint64_t n,
+                                           uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
+                                           hipStream_t stream);
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
@@ -1013,6 +1016,42 @@ int infw_pack_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_
         set_error(std::string("pack launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }
+    return 0;
+}
+
+int infw_classify_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n, uint32_t *result_words,
+                         uint8_t *xdp_verdicts, void *stream) {
+    if (!ctx || !fb) return -EINVAL;
+    if (ctx->devs.empty()) {
+        set_error("classify_frames: host-only context has no device tables");
+        return -ENODEV;
+    }
+    if (dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+    if (n && (!fb->frames || !fb->linear_len || !fb->ifindex || (!fb->offsets && !fb->stride))) {
+        set_error("classify_frames: bad arguments");
+        return -EINVAL;
+    }
+    Device &d = ctx->devs[dev];
+    std::shared_ptr<DeviceEpoch> ep;
+    {
+        std::lock_guard<std::mutex> lk(ctx->epoch_mu);
+        ep = d.epoch;
+    }
+    DeviceGuard g(d.ordinal);
+    if (!g.ok) {
+        set_error("hipSetDevice failed");
+        return -ENODEV;
+    }
+    if (ep->wait_ready(static_cast<hipStream_t>(stream))) {
+        set_error("classify_frames: stream wait on the epoch's upload failed");
+        return -EIO;
+    }
+    if (infw_launch_classify_frames(&ep->view, fb, n, result_words, xdp_verdicts, d.stats, d.cus,
+                                    static_cast<hipStream_t>(stream))) {
+        set_error(std::string("classify_frames launch failed: ") + hipGetErrorString(hipGetLastError()));
+        return -EIO;
+    }
+    ep->mark_use(static_cast<hipStream_t>(stream));
     return 0;
 }
 

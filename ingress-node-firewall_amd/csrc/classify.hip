@@ -233,7 +233,31 @@ struct BatchIn {
     const uint32_t *saddr4;  // compact layout
     const uint8_t *v6tail;
     const uint32_t *ifindex, *pkt_len, *meta, *l4word;
+    // raw frames (kF, infw_frame_batch): pkt_len may be null (= linear length); offsets null = fixed stride
+    const uint8_t *frames;
+    const uint64_t *offsets;
+    uint64_t fstride;
+    const uint32_t *linear_len;
 };
+
+// ---- raw frames (kF): the tuple of infw_pack_header() (infw_pack.h) built in the kernel from the frame's
+// header window, bytes [10, 58) — every byte kernel.c reads (ethertype :427, protocol :108/:115, saddr :204/:291,
+// the first L4 word at the fixed offset 34/54 :125-166).  A wave stages its 64 frames 16 at a time through a
+// 1-KiB LDS buffer of its own: lanes 4j..4j+3 load the four 16-B aligned chunks covering frame j's window (one
+// instruction moves 16 whole 64-B windows), then frame j's owner lane picks its fields out of LDS.  A chunk is
+// read only when it starts before min(linear length, 58), so frames packed back to back are never read past
+// their end; bytes at or past the linear length read as zero, as the packer's do.
+constexpr uint32_t kFrameWinWords = 17;  // 64-B window + 4 B: the 16 owners' reads spread over the banks
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+// Frame bytes [o, o + 4) from a staged window w whose byte 10 sits at position d, bytes >= cap as zero.
+__device__ __forceinline__ uint32_t frame_word(const uint32_t *w, uint32_t d, uint32_t o, uint32_t cap) {
+    const uint32_t p = o - 10u + d, q = p >> 2;
+    const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], p & 3u);
+    const int keep = (int)cap - (int)o;
+    return keep >= 4 ? x : keep <= 0 ? 0u : x & ((1u << (8 * keep)) - 1u);
+}
 
 // G > 0: one-lane-per-rule ballot scan with G packets in flight; G == 0: decision tables.
 struct EventSink {
@@ -299,7 +323,7 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128), bool kLean = false>
+          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -323,6 +347,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     // no access needs to be indivisible beyond 8 B.  The distinct C_j keep a zeroed entry from validating.
     constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
     __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
+    __shared__ uint32_t s_fw[kF ? kBlock / 64 : 1][kF ? 16 * kFrameWinWords : 1];  // per-wave frame windows
     if (kB6)
         for (int i = threadIdx.x; i < (int)(2u << kB6Log); i += kBlock) s_b6[i] = u32x4{0u, 0u, 0u, 0u};
     for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) {
@@ -346,6 +371,17 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     // the stream's latency overlaps the first table lookups instead of adding to them
     auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa,
                           bool with_meta = true) {
+        if (kF) {  // frames: linear length (meta), frame byte offset (sa.x/sa.y), ifindex, frame length
+            if (i < n) {
+                meta = __builtin_nontemporal_load(&in.linear_len[i]);
+                ifx = __builtin_nontemporal_load(&in.ifindex[i]);
+                plen = in.pkt_len ? __builtin_nontemporal_load(&in.pkt_len[i]) : meta;
+                const uint64_t off = in.offsets ? __builtin_nontemporal_load(&in.offsets[i]) : i * in.fstride;
+                sa.x = (uint32_t)off;
+                sa.y = (uint32_t)(off >> 32);
+            }
+            return;
+        }
         if (i < n) {
             if (!(kAblate & 16)) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL (16: plain, diagnostic)
                 if (with_meta) meta = __builtin_nontemporal_load(&in.meta[i]);
@@ -399,16 +435,64 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         const uint64_t i = base + threadIdx.x;
         const bool valid = i < n;
         if (!kPrefetch && base != (uint64_t)blockIdx.x * kBlock) load_tuple(i, n_meta, n_l4w, n_ifx, n_plen, n_sa);
-        const uint32_t meta = valid ? n_meta : 0, l4w = n_l4w, ifx = n_ifx, plen = n_plen;
+        uint32_t meta = valid ? n_meta : 0, l4w = n_l4w;
+        const uint32_t ifx = n_ifx, plen = n_plen;
         uint4 sa = n_sa;
-        if (kC && kPrefetch) {
+        if (kF) {
+            const uint32_t cap = meta;  // linear length (0 past the batch: nothing is read)
+            const uint64_t foff = (uint64_t)sa.y << 32 | sa.x;
+            if (kPrefetch) load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+            uint32_t *wb = s_fw[threadIdx.x >> 6];
+            u32x4 ch[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {  // round r: chunk (lane & 3) of the wave's frame 16r + (lane >> 2)
+                const uint32_t src = 16u * r + (lane >> 2);
+                const uint32_t c_cap = bperm(cap, src);
+                const uint64_t c_off = (uint64_t)bperm((uint32_t)(foff >> 32), src) << 32 | bperm((uint32_t)foff, src);
+                const uintptr_t f = (uintptr_t)(in.frames + c_off);
+                const uintptr_t at = ((f + 10u) & ~(uintptr_t)15) + 16u * (lane & 3u);
+                ch[r] = u32x4{0u, 0u, 0u, 0u};
+                if (c_cap > 10u && at < f + (c_cap < 58u ? c_cap : 58u))
+                    ch[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(at));
+            }
+            const uint32_t d = (uint32_t)(((uintptr_t)(in.frames + foff) + 10u) & 15u);
+            const uint32_t *w = wb + (lane & 15u) * kFrameWinWords;
+            uint32_t et = 0, proto = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0, l4 = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint32_t *dst = wb + (lane >> 2) * kFrameWinWords + 4u * (lane & 3u);
+                dst[0] = ch[r][0];
+                dst[1] = ch[r][1];
+                dst[2] = ch[r][2];
+                dst[3] = ch[r][3];
+                __builtin_amdgcn_wave_barrier();
+                if ((lane >> 4) == (uint32_t)r) {  // the round's 16 owners read their frames' fields
+                    const uint32_t e = frame_word(w, d, 12, cap);
+                    et = cap >= 14u ? (e & 0xFFu) << 8 | ((e >> 8) & 0xFFu) : 0u;
+                    const bool v4 = et == 0x0800u, v6 = et == 0x86DDu;
+                    const uint32_t f20 = frame_word(w, d, 20, cap);
+                    proto = v4 ? f20 >> 24 : v6 ? f20 & 0xFFu : 0u;
+                    s0 = v4 ? frame_word(w, d, 26, cap) : v6 ? frame_word(w, d, 22, cap) : 0u;
+                    l4 = v4 ? frame_word(w, d, 34, cap) : v6 ? frame_word(w, d, 54, cap) : 0u;
+                    if (v6) {
+                        s1 = frame_word(w, d, 26, cap);
+                        s2 = frame_word(w, d, 30, cap);
+                        s3 = frame_word(w, d, 34, cap);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // the next round rewrites the buffer
+            }
+            meta = et | proto << 16 | (cap > 255u ? 255u : cap) << 24;
+            l4w = l4;
+            sa = make_uint4(s0, s1, s2, s3);
+        } else if (kC && kPrefetch) {
             sa.y = n_t0;
             sa.z = n_t1;
             sa.w = n_t2;
         } else if (kC) {  // no prefetch (diagnostic 128): the tails load with the tile
             load_tail(i, meta, sa.y, sa.z, sa.w);
         }
-        if (kPrefetch) {
+        if (kPrefetch && !kF) {
             if (kC) {
                 const uint32_t m1 = n_meta2;  // tile t+1's meta, loaded one tile ago
                 load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa, false);
@@ -643,14 +727,15 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false>
+          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
+          bool kF = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -764,5 +849,24 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         else if (group == 4) launch<512, 4>(bpc, cus, T, in, n, results, verdicts, st, stream);
         else launch<512, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Classification straight from raw frames in HBM (infw_frame_batch; the packer's tuple is built in the kernel,
+// no SoA batch is written or read): 768 x 2 with a 2048-entry word cache, the LDS the frame windows need.
+extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_frame_batch *fb, uint64_t n,
+                                           uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
+                                           hipStream_t stream) {
+    if (n == 0) return 0;
+    BatchIn bi{};
+    bi.ifindex = fb->ifindex;
+    bi.pkt_len = fb->pkt_len;
+    bi.frames = fb->frames;
+    bi.offsets = fb->offsets;
+    bi.fstride = fb->stride;
+    bi.linear_len = fb->linear_len;
+    auto *st = reinterpret_cast<unsigned long long *>(stats);
+    if (T->lean) launch<768, 0, 0, false, 6, false, false, 11, 9, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    else launch<768, 0, 0, false, 6, false, false, 11, 9, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

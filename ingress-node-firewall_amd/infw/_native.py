@@ -135,7 +135,7 @@ ABI_SYMBOLS = [
     "infw_stats_bind", "infw_stats_device_ptr", "infw_build_ebpf_key", "infw_make_rule",
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
-    "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c",
+    "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c", "infw_classify_frames",
     "infw_get_launch", "infw_events_capture",
 ]
 
@@ -180,6 +180,8 @@ _sig = {
     "infw_classify_c": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoaC), C.c_uint64, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
     "infw_pack_frames_c": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoaC), C.c_void_p]),
+    "infw_classify_frames": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
     "infw_events_capture": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_uint64,
                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     "infw_soa_compact": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,

@@ -245,6 +245,21 @@ class Classifier:
                         out_c.pkt_len.data_ptr(), out_c.meta.data_ptr(), out_c.l4word.data_ptr())
         check(N.lib.infw_pack_frames_c(self._ctx, dev, C.byref(fb), out_c.n, C.byref(o), sp), "pack_frames_c")
 
+    def classify_frames(self, frames, linear_len, ifindex, n: int, results=None, verdicts=None, pkt_len=None,
+                        offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
+        """infw_classify_frames: classify n frames in device memory (uint8 tensor) without a SoA batch — the same
+        result words, verdicts and counters as pack_frames + classify."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        fb = N.FrameBatch(frames.data_ptr(), offsets.data_ptr() if offsets is not None else None, stride,
+                          linear_len.data_ptr(), pkt_len.data_ptr() if pkt_len is not None else None,
+                          ifindex.data_ptr())
+        check(N.lib.infw_classify_frames(self._ctx, dev, C.byref(fb), n,
+                                         results.data_ptr() if results is not None else None,
+                                         verdicts.data_ptr() if verdicts is not None else None, sp), "classify_frames")
+
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
         """The perf samples of the deny events classify_events wrote (kernel.c:392-399) from the frames the batch was

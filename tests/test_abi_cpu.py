@@ -47,6 +47,8 @@ def test_no_device_means_no_classifier():
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
     rc = N.lib.infw_classify(c._ctx, 0, C.byref(N.BatchSoa(1, 1, 1, 1, 1)), 1, None, None, None)
     assert rc == -19
+    rc = N.lib.infw_classify_frames(c._ctx, 0, C.byref(N.FrameBatch(1, None, 64, 1, None, 1)), 1, None, None, None)
+    assert rc == -19
 
 
 def key(plen, ifx, ip: bytes):

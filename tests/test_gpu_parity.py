@@ -387,6 +387,89 @@ def test_pack_frames_on_device():
         assert np.array_equal(res.cpu().numpy().view(np.uint32), g_std)
 
 
+def _frames_run(clf, dbuf, lens, fifx, n, dev, plen=None, offs=None, stride=0):
+    """infw_classify_frames over frames already on the device: (result words, verdicts, counters)."""
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    res = torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev)
+    ver = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device=dev)
+    kw = dict(stride=stride) if stride else dict(offsets=torch.from_numpy(offs.view(np.int64)).to(dev))
+    clf.stats_reset()
+    clf.classify_frames(dbuf, t(lens), t(fifx), n, results=res, verdicts=ver,
+                        pkt_len=t(plen) if plen is not None else None, **kw)
+    torch.cuda.synchronize()
+    return res.cpu().numpy().view(np.uint32)[:n], ver.cpu().numpy()[:n], clf.stats_read_all()
+
+
+@pytest.mark.parametrize("short_table", ["dir24", "compressed"])
+def test_classify_frames_on_device(monkeypatch, short_table):
+    """§8f-3 classification straight from raw frames (infw_classify_frames: the tuple is built in the kernel from
+    the staged header window): result words, verdicts and counters equal the oracle's on the same frames —
+    header snapshots at a fixed stride (a ragged count), and variable-length real frames back to back with an
+    offset array (truncated ones, the shortest at the very end of the buffer).  The compressed short table runs
+    the kernel's full (non-lean) instantiation."""
+    from frames import frame, snapshots
+    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
+    dev = torch.device("cuda", 0)
+    for cfg, npre, ntpl in ((W.CFG2_MIXED_1M, 50000, 256), (W.CFG4_ADVERSARIAL, 20000, 64)):
+        wl = W.Workload(cfg, n_prefixes=npre, n_templates=ntpl)
+        clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+        wl.load_into(clf)
+        clf.commit()
+        m = oracle_for(wl)
+        n = (1 << 18) + 77
+        hdr, cap, pl, ifx = wl.frames(7, n)
+        cap = np.minimum(cap, 80).astype(np.uint32)
+        gres, gver, gst = _frames_run(clf, torch.from_numpy(np.ascontiguousarray(hdr)).to(dev), cap, ifx, n, dev,
+                                      plen=pl, stride=80)
+        ores, over, ost, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+        assert np.array_equal(gres, ores) and np.array_equal(gver, over), cfg
+        assert np.array_equal(gst, ost), cfg
+    # variable-length real frames, back to back (frame bytes past each one's length belong to the next frame)
+    rng = np.random.default_rng(17)
+    fr = []
+    for k in range(5000):
+        src = "1.1.%d.%d" % (k & 255, (k >> 8) & 255) if k % 2 else "100:1::%x" % k
+        f = frame(src, proto=["tcp", "udp", "icmp", "icmpv6", "sctp", "gre"][k % 6], dport=int(rng.integers(0, 65536)),
+                  icmp_type=8, length=int(rng.integers(40, 300)))
+        fr.append(f[: int(rng.integers(0, len(f) + 1))] if k % 5 == 0 else f)
+    fr.append(frame("1.1.1.1", proto="tcp", dport=150)[:15])
+    offs = np.cumsum([0] + [len(f) for f in fr[:-1]]).astype(np.uint64)
+    buf = torch.from_numpy(np.frombuffer(b"".join(fr), np.uint8).copy()).to(dev)
+    lens = np.array([len(f) for f in fr], np.uint32)
+    ifs = np.where(np.arange(len(fr)) % 3 == 0, 2, 1).astype(np.uint32)
+    h2, c2, p2 = snapshots(fr)
+    gres, gver, gst = _frames_run(clf, buf, lens, ifs, len(fr), dev, offs=offs)
+    ores, over, ost, _ = m.classify_frames(h2, c2, p2, ifs, nthreads=2)
+    assert np.array_equal(gres, ores) and np.array_equal(gver, over) and np.array_equal(gst, ost)
+    # an empty batch launches nothing
+    gres, gver, gst = _frames_run(clf, buf, lens[:0], ifs[:0], 0, dev, offs=offs[:0])
+    assert not gst.any()
+
+
+def test_survey_probes_from_frames_on_device():
+    """Every survey probe (truncation at each header boundary, family gating, unified key space ...) as real frames
+    back to back through infw_classify_frames: verdicts, result words and counters as recorded."""
+    import goenc
+    from test_golden import expected_stats, load, probe_frames
+    dev = torch.device("cuda", 0)
+    for case in load("survey_probes.json")["cases"]:
+        c = infw.Classifier(devices=[0])
+        for e in case["table"]:
+            c.update(infw.build_ebpf_key(e["key"]["ifindex"], e["key"]["cidr"]),
+                     infw.RulesValSt.from_buffer_copy(goenc.raw_value(e["rules"])))
+        c.commit()
+        frames, ifx = probe_frames(case)
+        offs = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint64)
+        buf = torch.from_numpy(np.frombuffer(b"".join(frames) + b"\0" * 16, np.uint8).copy()).to(dev)
+        lens = np.array([len(f) for f in frames], np.uint32)
+        res, ver, st = _frames_run(c, buf, lens, np.array(ifx, np.uint32), len(frames), dev, offs=offs)
+        for p, v, r in zip(case["packets"], ver, res):
+            assert v == p["expect"]["retval"], (case["name"], p, v, hex(r))
+            if "result" in p["expect"]:
+                assert r == p["expect"]["result"], (case["name"], p, hex(r))
+        assert np.array_equal(st, expected_stats(case, frames)), case["name"]
+
+
 @pytest.mark.parametrize("short_table", ["dir24", "compressed"])
 def test_survey_probes_on_device(monkeypatch, short_table):
     """Every probe of tests/golden/survey_probes.json (the reference's edge semantics:
