@@ -439,13 +439,17 @@ struct infw_table_info {
     double compile_ms;         /* host compile time of the last commit        */
     double upload_ms;          /* H2D time of the last commit                 */
     uint64_t n_v6_groups;      /* (ifindex, /32) groups of IPv6 long prefixes */
-    uint64_t n_v6_overflow;    /* groups with > 3 long prefixes (Waldvogel)   */
+    uint64_t n_v6_overflow;    /* groups in the Waldvogel table (> 3 long      */
+                               /* prefixes; > 2 in the two-choice slot form)  */
     uint32_t commit_mode;      /* INFW_COMMIT_*: how the last commit ran      */
     uint32_t dt_parts;         /* value parts per (list, class) decision table */
     uint64_t patch_bytes;      /* bytes copied to the devices by it           */
     uint64_t dead_lists;       /* compiled lists no entry references (GC'd by */
                                /* the next full compile)                      */
     char full_reason[48];      /* why the last full compile was needed        */
+    uint64_t v6_slot_buckets;  /* != 0: IPv6 groups in the two-choice slot    */
+                               /* form, this many 64-B buckets (else one group */
+                               /* per bucket at <= 1/8 load)                   */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
 #define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */

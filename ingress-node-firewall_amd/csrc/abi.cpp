@@ -265,6 +265,7 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.n_slots = h.n_slots;
     t.lmask = h.ltab.size() - 1;
     t.bmask = h.btab.size() - 1;
+    t.b2n = h.b2n;
     t.short_mode = h.short_mode;
     t.n_levels = (uint32_t)h.levels.size();
     t.dt_plog2 = h.dt_plog2;
@@ -679,6 +680,7 @@ int infw_table_commit(infw_ctx *ctx) {
     in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     in.n_v6_groups = h.n_buckets;
     in.n_v6_overflow = h.n_overflow_groups;
+    in.v6_slot_buckets = h.b2n;
     in.commit_mode = mode;
     in.dt_parts = 1u << h.dt_plog2;
     in.patch_bytes = patched;

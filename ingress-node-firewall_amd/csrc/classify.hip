@@ -203,8 +203,46 @@ __device__ __forceinline__ uint32_t v6_finish(const infw_dev_tables &T, uint32_t
     }
 }
 
+// v6_finish over the two-choice slot form (infw_tables.h): slot 0 {h, r0} of bucket bi is loaded; slot 1 of the
+// same 64-B bucket only when slot 0 holds another group or a second record, the second bucket only when the
+// first is marked DISPLACED.
+template <bool kLean = false>
+__device__ __forceinline__ uint32_t v6_finish_b2(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
+                                                const uint32_t sa[4], uint64_t hash, uint64_t bi, u32x4 h, u32x4 r0) {
+    const uint32_t mid = infw_bswap32(sa[1]);
+    const uint64_t lo = infw_be64(sa[2], sa[3]);
+    for (int probe = 0;; probe++) {
+        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
+        if (h[0] == 0) {  // empty bucket (an emptied slot 0 keeps the bucket's DISPLACED flag)
+            if (probe || !(h[2] & INFW_B2_DISPLACED)) return 0;
+        } else if (h[0] == slot + 1 && h[1] == a32) {
+            const uint32_t nr = h[2] & 0xFFu;
+            if (nr == INFW_BUCKET_OVERFLOW) return kLean ? 0u : infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
+            if (infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
+            if (nr == 2) {
+                const u32x4 r1 = b[3];
+                if (infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo)) return r1[3] & 0x1FFFFFFu;
+            }
+            return 0;
+        } else {
+            const u32x4 h1 = b[2], r1 = b[3];
+            if (h1[0] == slot + 1 && h1[1] == a32) {  // a one-record (or overflowed) group in slot 1
+                if ((h1[2] & 0xFFu) == INFW_BUCKET_OVERFLOW)
+                    return kLean ? 0u : infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
+                return infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo) ? r1[3] & 0x1FFFFFFu : 0u;
+            }
+            if (probe || !(h[2] & INFW_B2_DISPLACED)) return 0;
+        }
+        bi = INFW_B2_INDEX(hash, T.b2n);
+        const u32x4 *b2 = reinterpret_cast<const u32x4 *>(T.btab + bi);
+        h = b2[0];
+        r0 = b2[1];
+    }
+}
+
 __device__ __forceinline__ uint32_t v6_long_dev(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                 const uint32_t sa[4]) {
+    if (T.b2n) return infw_v6_long(T, slot, a32, sa);
     const uint32_t mid = infw_bswap32(sa[1]);
     const uint64_t lo = infw_be64(sa[2], sa[3]);
     uint64_t i = infw_bucket_hash(slot, a32) & T.bmask;
@@ -323,13 +361,15 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false>
+          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
                                                           const Sideband sb) {
     const EventSink &ev = sb.ev;
+    // IPv6 group table form: kV6 0 = one group per bucket, 1 = two-choice slots, 2 = whichever the epoch has
+    const bool b2 = kV6 == 2 ? T.b2n != 0 : kV6 == 1;
     __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
     __shared__ unsigned long long s_by[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
@@ -584,13 +624,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
                     if (need6) {
-                        bi = bhash & T.bmask;
+                        bi = b2 ? INFW_B2_INDEX(bhash >> 32, T.b2n) : bhash & T.bmask;
                         const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
                         bh = b[0];
                         br0 = b[1];
                     }
                     if (need6) {
-                        lng = v6_finish<kLean>(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                        lng = b2 ? v6_finish_b2<kLean>(T, (uint32_t)slot, a32, sw, bhash, bi, bh, br0)
+                                    : v6_finish<kLean>(T, (uint32_t)slot, a32, sw, bi, bh, br0);
                         if (b6ok && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
                             s_b6[2 * b6idx] = u32x4{b6tag ^ kB6C0, br0[0], b6tag ^ kB6C1, br0[1]};
                             s_b6[2 * b6idx + 1] = u32x4{b6tag ^ kB6C2, br0[2], b6tag ^ kB6C3, br0[3]};
@@ -728,14 +769,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false>
+          bool kF = false, int kV6 = 2>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -753,9 +794,15 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)  // the default shape without the rare paths
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6) launch<768, 0, 0, false, 6, false, kC, 12, 9>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && !T->b2n)
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, false, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6)
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, false, false, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else return false;
     return true;

@@ -110,6 +110,7 @@ struct HostTables {
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;
     uint64_t n_buckets = 0, n_overflow_groups = 0;
+    uint64_t b2n = 0;                   // != 0: btab in the two-choice slot form (infw_tables.h) with b2n buckets
     std::vector<uint32_t> wild{0u, 0u, 0u};  // prefixLen < 32 entries: {plen, key bits, list+1}, longest first
     uint32_t n_wild = 0;
     std::vector<uint8_t> levels;

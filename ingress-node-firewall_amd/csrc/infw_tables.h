@@ -77,6 +77,27 @@ struct infw_v6_bucket {     // 64 B
     struct infw_v6_rec rec[INFW_BUCKET_INLINE];
 };
 
+// Two-choice slot form of the same groups (v6_form B2, b2n = bucket count != 0): chosen per full compile
+// when the groups fit a bucket table of at most INFW_B2_BUDGET bytes (the XCD L2s' scale), because the
+// one-group-per-bucket form at 1/8 load spreads a small group set over twice the 128-B lines it fills.  A
+// 64-B bucket holds two 32-B slots {tag, top, info, pad, record}; a group of one record takes one slot, a
+// group of two records both slots of one bucket (longest first), a larger group one slot with n =
+// INFW_BUCKET_OVERFLOW (Waldvogel table).  A group lives in bucket i1 or — when i1 was full — i2 (two
+// halves of one hash, range-reduced), and then i1's slot 0 carries INFW_B2_DISPLACED, so a lookup reads a
+// second bucket only for groups (or absent keys) whose first bucket overflowed.  Slot 1 is used only when
+// slot 0 is (an incremental removal moves slot 1 down); an emptied slot 0 keeps the bucket's DISPLACED flag.
+struct infw_v6_slot {       // 32 B
+    uint32_t tag;           // slot + 1, 0 = empty
+    uint32_t top;           // address bits 0..31
+    uint32_t info;          // records of the group (1, 2) or INFW_BUCKET_OVERFLOW; slot 0: | INFW_B2_DISPLACED
+    uint32_t pad;
+    struct infw_v6_rec rec;
+};
+#define INFW_B2_DISPLACED 0x80000000u
+#define INFW_B2_BUDGET (8ull << 20)
+// bucket index of a 32-bit hash half in [0, nb)
+#define INFW_B2_INDEX(h32, nb) ((uint64_t)(uint32_t)(h32) * (uint64_t)(nb) >> 32)
+
 // First-match decision tables.  For one (rule list, packet class) the
 // first-match result as a function of the 16-bit packet value (dport, or
 // type << 8 | code) is a step function with S <= 2c + 1 <= 201 segments.  The
@@ -156,6 +177,7 @@ struct infw_dev_tables {
     uint32_t n_wild;           // longest first; consulted for ifindexes without a slot (their own entries)
     uint32_t lean;             // 1: no compressed short table, no overflowed IPv6 group, no partial-ifindex prefix —
                                // the kernel may launch without those code paths (fewer live registers)
+    uint64_t b2n;              // != 0: btab holds the two-choice slot form with this many buckets
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -445,12 +467,35 @@ INFW_TD uint32_t infw_long_lookup(const T &t, uint32_t slot, uint64_t hi, uint64
     return best;
 }
 
+// infw_v6_long over the two-choice slot form.
+template <class T>
+INFW_TD uint32_t infw_v6_long_b2(const T &t, uint32_t slot, uint32_t a32, uint32_t mid, uint64_t lo) {
+    const uint64_t h = infw_bucket_hash(slot, a32);
+    const struct infw_v6_slot *s = (const struct infw_v6_slot *)(const void *)t.btab;
+    for (int probe = 0; probe < 2; probe++) {
+        const struct infw_v6_slot *b = s + 2 * INFW_B2_INDEX(probe ? h : h >> 32, t.b2n);
+        for (int k = 0; k < 2; k++) {
+            if (b[k].tag == slot + 1 && b[k].top == a32) {
+                const uint32_t nr = b[k].info & 0xFFu;
+                if (nr == INFW_BUCKET_OVERFLOW) return infw_long_lookup(t, slot, (uint64_t)a32 << 32 | mid, lo);
+                if (infw_rec_match(b[k].rec.mid, b[k].rec.lo, b[k].rec.meta, mid, lo)) return b[k].rec.meta & 0x1FFFFFFu;
+                if (nr == 2 && k == 0 && infw_rec_match(b[1].rec.mid, b[1].rec.lo, b[1].rec.meta, mid, lo))
+                    return b[1].rec.meta & 0x1FFFFFFu;
+                return 0;
+            }
+        }
+        if (!(b[0].info & INFW_B2_DISPLACED)) return 0;  // (an emptied slot 0 keeps the bucket's flag)
+    }
+    return 0;
+}
+
 // Longest long (/33../128) prefix covering an IPv6 address: its /32 group's
 // bucket, or the Waldvogel table when the group overflowed.  list+1 or 0.
 template <class T>
 INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uint32_t sa[4]) {
     const uint32_t mid = infw_bswap32(sa[1]);
     const uint64_t lo = infw_be64(sa[2], sa[3]);
+    if (t.b2n) return infw_v6_long_b2(t, slot, a32, mid, lo);
     uint64_t i = infw_bucket_hash(slot, a32) & t.bmask;
     for (;;) {
         const struct infw_v6_bucket *b = &t.btab[i];

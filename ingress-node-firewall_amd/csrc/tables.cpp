@@ -954,16 +954,118 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             g.recs.push_back(infw_v6_rec{r.lo, (uint32_t)r.hi, (r.len - 32) << 25 | r.list1});
         }
+        // the two-choice slot form (infw_tables.h) when the groups fit INFW_B2_BUDGET (from 70 % slot load, the
+        // table grown by 1/8 while a cuckoo placement fails);
+        // INFW_V6_FORM=b2|std forces a form (b2 grows the table until every group is placed)
+        {
+            const char *fe = getenv("INFW_V6_FORM");
+            const bool force_b2 = fe && !strcmp(fe, "b2"), force_std = fe && !strcmp(fe, "std");
+            std::vector<uint64_t> keys;
+            keys.reserve(groups.size());
+            uint64_t slots = 0;
+            for (const auto &kv : groups) {
+                keys.push_back(kv.first);
+                slots += kv.second.recs.size() == 2 ? 2 : 1;
+            }
+            std::sort(keys.begin(), keys.end());
+            uint64_t nb = std::max<uint64_t>(64, (slots * 5 + 6) / 7);  // 2 slots per bucket at 70 % load
+            const bool want = !groups.empty() && !force_std && (force_b2 || nb * 64 <= INFW_B2_BUDGET);
+            for (int attempt = 0; want && attempt < 8 && (force_b2 || nb * 64 <= INFW_B2_BUDGET); attempt++, nb += nb / 8) {
+                std::vector<infw_v6_slot> tab(2 * nb);
+                memset(tab.data(), 0, tab.size() * sizeof(infw_v6_slot));
+                auto idx = [&](const G &g, int which) {
+                    const uint64_t h = infw_bucket_hash(g.slot, g.top);
+                    return which ? INFW_B2_INDEX(h, nb) : INFW_B2_INDEX(h >> 32, nb);
+                };
+                auto need_of = [](const G &g) -> uint32_t { return g.recs.size() == 2 ? 2u : 1u; };
+                auto put = [&](uint64_t i, G &g) {  // into bucket i's free slots, or false
+                    infw_v6_slot *b = &tab[2 * i];
+                    const uint32_t k = b[0].tag == 0 ? 0 : b[1].tag == 0 ? 1 : 2, need = need_of(g);
+                    if (k + need > 2) return false;
+                    if (g.recs.size() > 2) {
+                        b[k].info = INFW_BUCKET_OVERFLOW;
+                    } else {
+                        std::sort(g.recs.begin(), g.recs.end(),
+                                  [](const infw_v6_rec &x, const infw_v6_rec &y) { return x.meta > y.meta; });
+                        for (uint32_t j = 0; j < need; j++) {
+                            b[k + j].info = (uint32_t)g.recs.size();
+                            b[k + j].rec = g.recs[j];
+                        }
+                    }
+                    for (uint32_t j = 0; j < need; j++) {
+                        b[k + j].tag = g.slot + 1;
+                        b[k + j].top = g.top;
+                    }
+                    return true;
+                };
+                // cuckoo insertion: a group that finds both buckets full evicts the groups of one of them
+                // (chosen by a fixed-seed generator), which are re-inserted in turn, up to a step limit
+                uint64_t rng = 0x9E3779B97F4A7C15ull, steps = 0;
+                const uint64_t max_steps = 64 * groups.size() + 1024;
+                bool ok = true;
+                std::vector<uint64_t> pending;
+                for (int pass = 0; pass < 2 && ok; pass++)  // two-record groups (a whole bucket) first
+                    for (uint64_t key : keys) {
+                        if ((groups[key].recs.size() == 2) != (pass == 0)) continue;
+                        pending.push_back(key);
+                        while (!pending.empty() && ok) {
+                            const uint64_t cur = pending.back();
+                            pending.pop_back();
+                            G &g = groups[cur];
+                            if (put(idx(g, 0), g) || put(idx(g, 1), g)) continue;
+                            if (++steps > max_steps) {
+                                ok = false;
+                                break;
+                            }
+                            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+                            const uint64_t v = idx(g, (int)(rng >> 63));
+                            infw_v6_slot *b = &tab[2 * v];
+                            const bool pair = b[0].tag == b[1].tag && b[0].top == b[1].top;  // one two-slot group
+                            if (need_of(g) == 2 || pair) {  // evict the bucket's groups (a two-slot group once)
+                                for (int k = 0; k < (pair ? 1 : 2); k++)
+                                    if (b[k].tag) pending.push_back((uint64_t)(b[k].tag - 1) << 32 | b[k].top);
+                                b[0] = b[1] = infw_v6_slot{};
+                            } else {  // one slot, chosen at random: the other group stays (moved to slot 0)
+                                const int k = (int)(rng >> 62) & 1;
+                                pending.push_back((uint64_t)(b[k].tag - 1) << 32 | b[k].top);
+                                if (k == 0) b[0] = b[1];
+                                b[0].info &= ~INFW_B2_DISPLACED;
+                                b[1] = infw_v6_slot{};
+                            }
+                            put(v, g);
+                        }
+                    }
+                if (ok)  // a group living in its second bucket marks its first one
+                    for (uint64_t i = 0; i < nb; i++)
+                        for (int k = 0; k < 2; k++) {
+                            const infw_v6_slot &sl = tab[2 * i + k];
+                            if (!sl.tag || (k == 1 && tab[2 * i].tag == sl.tag && tab[2 * i].top == sl.top)) continue;
+                            const uint64_t i1 = idx(groups[(uint64_t)(sl.tag - 1) << 32 | sl.top], 0);
+                            if (i1 != i) tab[2 * i1].info |= INFW_B2_DISPLACED;
+                        }
+                if (trace)
+                    fprintf(stderr, "[compile] IPv6 slot form: %zu groups, %llu slots, %llu buckets: %s\n", groups.size(),
+                            (unsigned long long)slots, (unsigned long long)nb, ok ? "placed" : "placement failed");
+                if (!ok) continue;
+                out.btab.assign(nb, infw_v6_bucket{});
+                memcpy(out.btab.data(), tab.data(), nb * sizeof(infw_v6_bucket));
+                out.b2n = nb;
+                for (const auto &kv : groups) out.n_overflow_groups += kv.second.recs.size() > 2;
+                break;
+            }
+        }
         // a wave waits for its slowest lane's probe chain: keep the load at or below 1/8
         // (INFW_BUCKET_SPREAD=k: capacity >= k x groups), the untouched capacity costs no cache
         uint64_t spread = 8;
         if (const char *e = getenv("INFW_BUCKET_SPREAD")) spread = std::max(2, atoi(e));
         uint64_t cap = 1024;
         while (cap < groups.size() * spread) cap <<= 1;
-        out.btab.assign(cap, infw_v6_bucket{});
-        memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
+        if (out.b2n) cap = 0;  // placed in the slot form above
+        if (cap) out.btab.assign(cap, infw_v6_bucket{});
+        if (cap) memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
         const uint64_t bmask = cap - 1;
         for (auto &kv : groups) {
+            if (!cap) break;
             G &g = kv.second;
             uint64_t i = infw_bucket_hash(g.slot, g.top) & bmask;
             while (out.btab[i].tag) i = (i + 1) & bmask;
@@ -1060,6 +1162,7 @@ infw_dev_tables HostTables::view() const {
     t.lmask = ltab.size() - 1;
     t.btab = btab.data();
     t.bmask = btab.size() - 1;
+    t.b2n = b2n;
     t.desc = desc.data();
     t.rules = rules.data();
     t.dte = dte.data();

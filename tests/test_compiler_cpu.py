@@ -33,11 +33,20 @@ def walk_vs_oracle(entries, tuples_from, n=20000, seed=1):
     return c, res
 
 
-@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG0_DEMO, 0, 0), (W.CFG1_V4_10K, 0, 0),
-                                            (W.CFG2_MIXED_1M, 100000, 512), (W.CFG4_ADVERSARIAL, 20000, 64)])
-def test_workloads(cfg, npfx, ntmpl):
+@pytest.mark.parametrize("cfg,npfx,ntmpl,v6_form", [(W.CFG0_DEMO, 0, 0, ""), (W.CFG1_V4_10K, 0, 0, ""),
+                                                    (W.CFG2_MIXED_1M, 100000, 512, "std"),
+                                                    (W.CFG2_MIXED_1M, 100000, 512, "b2"),
+                                                    (W.CFG4_ADVERSARIAL, 20000, 64, "std"),
+                                                    (W.CFG4_ADVERSARIAL, 20000, 64, "b2")])
+def test_workloads(monkeypatch, cfg, npfx, ntmpl, v6_form):
+    """The host walk of the compiled image equals the oracle; IPv6 groups in either bucket form
+    (INFW_V6_FORM: one group per bucket, or the two-choice slot form)."""
+    if v6_form:
+        monkeypatch.setenv("INFW_V6_FORM", v6_form)
     wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
-    walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
+    c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
+    if v6_form:
+        assert (c.info()["v6_slot_buckets"] > 0) == (v6_form == "b2")
 
 
 def test_distinct_lists_parallel_compile(monkeypatch):
@@ -97,7 +106,9 @@ def _clustered_table(rng, n_groups=40):
     return out, anchors
 
 
-def test_clustered_overflow_groups():
+@pytest.mark.parametrize("v6_form", ["std", "b2"])
+def test_clustered_overflow_groups(monkeypatch, v6_form):
+    monkeypatch.setenv("INFW_V6_FORM", v6_form)
     rng = random.Random(7)
     entries, anchors = _clustered_table(rng)
     from frames import frame, snapshots
@@ -129,8 +140,10 @@ def test_clustered_overflow_groups():
     assert (res != 0).mean() > 0.3
 
 
-def test_update_delete_churn_matches_oracle():
+@pytest.mark.parametrize("v6_form", ["std", "b2"])
+def test_update_delete_churn_matches_oracle(monkeypatch, v6_form):
     """Random update/delete/commit churn: the compiled image tracks the map exactly."""
+    monkeypatch.setenv("INFW_V6_FORM", v6_form)
     rng = random.Random(11)
     entries, anchors = _clustered_table(rng, n_groups=15)
     c = infw.Classifier(flags=infw.F_HOST_ONLY)

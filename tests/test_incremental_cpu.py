@@ -8,6 +8,7 @@ import random
 import struct
 
 import numpy as np
+import pytest
 
 import infw
 import orc
@@ -66,7 +67,11 @@ def _check(ctxs, m, hdr, cap, pl, ifx, what):
         assert bad.size == 0, (what, c.info()["commit_mode"], bad[:5], got[bad[:5]], want[bad[:5]])
 
 
-def test_incremental_churn_matches_oracle_and_full():
+@pytest.mark.parametrize("v6_form", ["std", "b2"])
+def test_incremental_churn_matches_oracle_and_full(monkeypatch, v6_form):
+    """Random edit batches, each committed incrementally (or by the fallback) and fully: both images walk like
+    the oracle, in either IPv6 bucket form (b2: new groups take free slots, removed ones free them)."""
+    monkeypatch.setenv("INFW_V6_FORM", v6_form)
     rng = random.Random(23)
     entries, anchors = _clustered_table(rng, n_groups=30)
     inc = infw.Classifier(flags=infw.F_HOST_ONLY)

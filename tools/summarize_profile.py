@@ -40,6 +40,8 @@ def main():
     stream_b = 32.0  # tuple bytes read per packet
     if layout == "compact":
         stream_b = line["roofline"]["algorithmic_bytes_per_packet"] - 4
+    elif layout == "frames":  # infw_classify_frames: the 12 B of length/ifindex streams; the 64-B frame windows
+        stream_b = 12.0       # (one per frame at the frame stride) are counted at face value, like gathers
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in ("kt/kt_kernel_stats.csv", "kt/kt_domain_stats.csv"):
