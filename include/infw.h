@@ -319,6 +319,12 @@ struct infw_classify_ex {
 int infw_classify_ex(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
                      uint32_t *result_words, uint8_t *xdp_verdicts,
                      const struct infw_classify_ex *ex, void *stream);
+/* infw_classify_frames with the sidebands: the event records' pkt_index is   */
+/* the frame's index in the batch, so infw_events_capture over the same       */
+/* frames writes the perf samples.                                            */
+int infw_classify_frames_ex(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
+                            uint32_t *result_words, uint8_t *xdp_verdicts,
+                            const struct infw_classify_ex *ex, void *stream);
 
 /*  - Deny-event payload: the perf sample each record stands for, as the      */
 /*    reader receives it (kernel.c:392-399: bpf_perf_event_output(ctx, map,   */

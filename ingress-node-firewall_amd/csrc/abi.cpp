@@ -19,7 +19,9 @@
 
 extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_frame_batch *fb, uint64_t n,
                                            uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                           hipStream_t stream);
+                                           hipStream_t stream, infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
+                                           uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count,
+                                           uint32_t dbg_slots);
 extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in, uint64_t n,
                                     uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
                                     int block, int group, int blocks_per_cu, hipStream_t stream,
@@ -1023,6 +1025,16 @@ int infw_pack_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_
 
 int infw_classify_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n, uint32_t *result_words,
                          uint8_t *xdp_verdicts, void *stream) {
+    return infw_classify_frames_ex(ctx, dev, fb, n, result_words, xdp_verdicts, nullptr, stream);
+}
+
+int infw_classify_frames_ex(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uint64_t n, uint32_t *result_words,
+                            uint8_t *xdp_verdicts, const struct infw_classify_ex *ex, void *stream) {
+    if (ex && (ex->size < sizeof(struct infw_classify_ex) || ex->flags != 0 || (ex->events_cap && !ex->events) ||
+               (ex->events && !ex->events_count))) {
+        set_error("classify_frames_ex: bad options");
+        return -EINVAL;
+    }
     if (!ctx || !fb) return -EINVAL;
     if (ctx->devs.empty()) {
         set_error("classify_frames: host-only context has no device tables");
@@ -1048,8 +1060,11 @@ int infw_classify_frames(infw_ctx *ctx, int dev, const infw_frame_batch *fb, uin
         set_error("classify_frames: stream wait on the epoch's upload failed");
         return -EIO;
     }
+    const bool evs = ex && ex->events_count;
     if (infw_launch_classify_frames(&ep->view, fb, n, result_words, xdp_verdicts, d.stats, d.cus,
-                                    static_cast<hipStream_t>(stream))) {
+                                    static_cast<hipStream_t>(stream), evs ? ex->events : nullptr,
+                                    evs ? ex->events_cap : 0, evs ? ex->events_count : nullptr,
+                                    ctx->debug_lookup ? d.dbg_fp : nullptr, d.dbg_keys, d.dbg_count, kDbgSlots)) {
         set_error(std::string("classify_frames launch failed: ") + hipGetErrorString(hipGetLastError()));
         return -EIO;
     }

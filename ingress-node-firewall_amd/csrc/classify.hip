@@ -901,9 +901,12 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
 
 // Classification straight from raw frames in HBM (infw_frame_batch; the packer's tuple is built in the kernel,
 // no SoA batch is written or read): 768 x 2 with a 2048-entry word cache, the LDS the frame windows need.
+// Sidebands (deny events, debug lookup capture) run 512 x 3 with them compiled in, like infw_launch_classify's.
 extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_frame_batch *fb, uint64_t n,
                                            uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                           hipStream_t stream) {
+                                           hipStream_t stream, infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
+                                           uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count,
+                                           uint32_t dbg_slots) {
     if (n == 0) return 0;
     BatchIn bi{};
     bi.ifindex = fb->ifindex;
@@ -913,6 +916,17 @@ extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_
     bi.fstride = fb->stride;
     bi.linear_len = fb->linear_len;
     auto *st = reinterpret_cast<unsigned long long *>(stats);
+    if (ev_count || dbg_fp) {
+        const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
+                          DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
+        if (ev_count && dbg_fp)
+            launch<512, 0, 0, true, 6, true, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
+        else if (ev_count)
+            launch<512, 0, 0, true, 6, false, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
+        else
+            launch<512, 0, 0, false, 6, true, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     if (T->lean) launch<768, 0, 0, false, 6, false, false, 11, 9, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     else launch<768, 0, 0, false, 6, false, false, 11, 9, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     return hipGetLastError() == hipSuccess ? 0 : -5;

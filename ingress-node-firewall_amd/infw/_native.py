@@ -136,6 +136,7 @@ ABI_SYMBOLS = [
     "infw_table_info", "infw_debug_walk", "infw_set_launch", "infw_last_error", "infw_abi_version",
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c", "infw_classify_frames",
+    "infw_classify_frames_ex",
     "infw_get_launch", "infw_events_capture",
 ]
 
@@ -182,6 +183,8 @@ _sig = {
     "infw_pack_frames_c": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, P(BatchSoaC), C.c_void_p]),
     "infw_classify_frames": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
+    "infw_classify_frames_ex": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_void_p,
+                                          P(ClassifyEx), C.c_void_p]),
     "infw_events_capture": (C.c_int, [C.c_void_p, C.c_int, P(FrameBatch), C.c_uint64, C.c_void_p, C.c_uint64,
                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     "infw_soa_compact": (C.c_int, [C.c_void_p, C.c_int, P(BatchSoa), C.c_uint64, C.c_void_p, C.c_void_p,

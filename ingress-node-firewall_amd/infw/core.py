@@ -246,9 +246,10 @@ class Classifier:
         check(N.lib.infw_pack_frames_c(self._ctx, dev, C.byref(fb), out_c.n, C.byref(o), sp), "pack_frames_c")
 
     def classify_frames(self, frames, linear_len, ifindex, n: int, results=None, verdicts=None, pkt_len=None,
-                        offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
+                        offsets=None, stride: int = 0, dev: int = 0, stream=None, events=None, events_count=None) -> None:
         """infw_classify_frames: classify n frames in device memory (uint8 tensor) without a SoA batch — the same
-        result words, verdicts and counters as pack_frames + classify."""
+        result words, verdicts and counters as pack_frames + classify.  events / events_count: the deny-event
+        stream as in classify_events (infw_classify_frames_ex)."""
         if stream is None:
             import torch
             stream = torch.cuda.current_stream(frames.device)
@@ -256,9 +257,14 @@ class Classifier:
         fb = N.FrameBatch(frames.data_ptr(), offsets.data_ptr() if offsets is not None else None, stride,
                           linear_len.data_ptr(), pkt_len.data_ptr() if pkt_len is not None else None,
                           ifindex.data_ptr())
-        check(N.lib.infw_classify_frames(self._ctx, dev, C.byref(fb), n,
-                                         results.data_ptr() if results is not None else None,
-                                         verdicts.data_ptr() if verdicts is not None else None, sp), "classify_frames")
+        ex = None
+        if events is not None:
+            ex = N.ClassifyEx(C.sizeof(N.ClassifyEx), 0, events.data_ptr(), events.numel() // C.sizeof(N.EventRec),
+                              events_count.data_ptr())
+        check(N.lib.infw_classify_frames_ex(self._ctx, dev, C.byref(fb), n,
+                                            results.data_ptr() if results is not None else None,
+                                            verdicts.data_ptr() if verdicts is not None else None,
+                                            C.byref(ex) if ex is not None else None, sp), "classify_frames")
 
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:

@@ -446,6 +446,49 @@ def test_classify_frames_on_device(monkeypatch, short_table):
     assert not gst.any()
 
 
+def test_frames_event_samples():
+    """Deny events from infw_classify_frames_ex (the frames kernel with the event sideband): the records equal the
+    packer path's (classify_events over the packed batch) after ordering by packet index, and
+    infw_events_capture over the same frames writes the oracle's perf samples (kernel.c:392-399)."""
+    import ctypes as C
+    from infw import _native as N
+    dev = torch.device("cuda", 0)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    for buf, offs, lens, plen, fifx, stride in event_frames(wl):
+        n = len(offs)
+        dbuf = torch.from_numpy(np.ascontiguousarray(buf).copy()).to(dev)
+        fkw = dict(stride=stride) if stride else dict(offsets=torch.from_numpy(offs.view(np.int64)).to(dev))
+        batch = SoaBatch.empty(n, dev)
+        clf.pack_frames(dbuf, t(lens), t(fifx), batch, pkt_len=t(plen), **fkw)
+        want_rec, want = m.collect_event_samples(buf, offs, lens, plen, fifx)
+        recs = []
+        for fused in (False, True):
+            ev = torch.zeros(n * C.sizeof(N.EventRec), dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            res = torch.empty(n, dtype=torch.int32, device=dev)
+            if fused:
+                clf.classify_frames(dbuf, t(lens), t(fifx), n, results=res, pkt_len=t(plen), events=ev,
+                                    events_count=cnt, **fkw)
+            else:
+                clf.classify_events(batch, ev, cnt, results=res)
+            smp = torch.zeros((n * N.EVENT_SAMPLE_BYTES,), dtype=torch.uint8, device=dev)
+            clf.events_capture(dbuf, t(lens), t(fifx), n, ev, cnt, smp, pkt_len=t(plen), **fkw)
+            torch.cuda.synchronize()
+            k = int(cnt.item())
+            r = ev.cpu().numpy().view(np.uint64).reshape(-1, 3)[:k]
+            order = np.argsort(r[:, 2], kind="stable")
+            recs.append((k, r[order], smp.cpu().numpy().reshape(-1, N.EVENT_SAMPLE_BYTES)[:k][order],
+                         res.cpu().numpy()))
+        assert recs[0][0] == recs[1][0] == want_rec.shape[0] > 200
+        assert np.array_equal(recs[0][1], recs[1][1]) and np.array_equal(recs[0][3], recs[1][3])
+        assert np.array_equal(recs[1][2], want)
+
+
 def test_survey_probes_from_frames_on_device():
     """Every survey probe (truncation at each header boundary, family gating, unified key space ...) as real frames
     back to back through infw_classify_frames: verdicts, result words and counters as recorded."""

@@ -17,6 +17,7 @@ run cfg4 --cfg 4 --no-cpu-baseline --steps 30
 run cfg2_uniform --uniform --no-cpu-baseline --steps 30
 run cfg2_distinct --templates 1000000 --no-cpu-baseline --steps 20
 run cfg2_frames --from-frames 128 --no-cpu-baseline --steps 20
+run cfg2_frames_fused --from-frames 128 --fused --no-cpu-baseline --steps 20
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
 for f in $OUT/*.log; do
   python3 -c "import json; l=[x for x in open('$f') if x.startswith('{')]; d=json.loads(l[-1]); r=d['roofline']; print('$(basename $f .log)', d['value'], r['kernel_ms_avg'], r['frac'], r.get('from_frames', {}).get('pack_kernel_ms_avg', ''))"
