@@ -77,9 +77,9 @@ struct infw_v6_bucket {     // 64 B
     struct infw_v6_rec rec[INFW_BUCKET_INLINE];
 };
 
-// Two-choice slot form of the same groups (v6_form B2, b2n = bucket count != 0): chosen per full compile
-// when the groups fit a bucket table of at most INFW_B2_BUDGET bytes (the XCD L2s' scale), because the
-// one-group-per-bucket form at 1/8 load spreads a small group set over twice the 128-B lines it fills.  A
+// Two-choice slot form of the same groups (b2n = bucket count != 0), an opt-in alternative (INFW_V6_FORM=b2;
+// measured slower than the form above at configs[4], tables.cpp): it packs a group set into fewer 128-B lines
+// than one group per bucket at 1/8 load, for a table that could stay in the XCD L2s.  A
 // 64-B bucket holds two 32-B slots {tag, top, info, pad, record}; a group of one record takes one slot, a
 // group of two records both slots of one bucket (longest first), a larger group one slot with n =
 // INFW_BUCKET_OVERFLOW (Waldvogel table).  A group lives in bucket i1 or — when i1 was full — i2 (two
@@ -94,7 +94,6 @@ struct infw_v6_slot {       // 32 B
     struct infw_v6_rec rec;
 };
 #define INFW_B2_DISPLACED 0x80000000u
-#define INFW_B2_BUDGET (8ull << 20)
 // bucket index of a 32-bit hash half in [0, nb)
 #define INFW_B2_INDEX(h32, nb) ((uint64_t)(uint32_t)(h32) * (uint64_t)(nb) >> 32)
 

@@ -954,12 +954,14 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             g.recs.push_back(infw_v6_rec{r.lo, (uint32_t)r.hi, (r.len - 32) << 25 | r.list1});
         }
-        // the two-choice slot form (infw_tables.h) when the groups fit INFW_B2_BUDGET (from 70 % slot load, the
-        // table grown by 1/8 while a cuckoo placement fails);
-        // INFW_V6_FORM=b2|std forces a form (b2 grows the table until every group is placed)
+        // the two-choice slot form (infw_tables.h) only when INFW_V6_FORM=b2 asks for it: from 70 % slot load,
+        // the table grown by 1/8 while a cuckoo placement fails.  Measured slower than one group per bucket at
+        // configs[4], the workload it was built for (3.99 vs 3.85 ms, profiles/r02h3/ab_v6form_cfg4.txt): the
+        // two-record groups hold the placement to ~50 % slot load (6.8 MB for 80k groups), and slot-1 and
+        // second-bucket reads cost more than the misses the denser table saves.
         {
             const char *fe = getenv("INFW_V6_FORM");
-            const bool force_b2 = fe && !strcmp(fe, "b2"), force_std = fe && !strcmp(fe, "std");
+            const bool force_b2 = fe && !strcmp(fe, "b2"), force_std = !force_b2;
             std::vector<uint64_t> keys;
             keys.reserve(groups.size());
             uint64_t slots = 0;
@@ -969,8 +971,8 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             std::sort(keys.begin(), keys.end());
             uint64_t nb = std::max<uint64_t>(64, (slots * 5 + 6) / 7);  // 2 slots per bucket at 70 % load
-            const bool want = !groups.empty() && !force_std && (force_b2 || nb * 64 <= INFW_B2_BUDGET);
-            for (int attempt = 0; want && attempt < 8 && (force_b2 || nb * 64 <= INFW_B2_BUDGET); attempt++, nb += nb / 8) {
+            const bool want = !groups.empty() && !force_std;
+            for (int attempt = 0; want && attempt < 8; attempt++, nb += nb / 8) {
                 std::vector<infw_v6_slot> tab(2 * nb);
                 memset(tab.data(), 0, tab.size() * sizeof(infw_v6_slot));
                 auto idx = [&](const G &g, int which) {

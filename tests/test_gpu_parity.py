@@ -319,6 +319,17 @@ def test_device_frame_generator():
     assert np.array_equal(ifx.cpu().numpy().view(np.uint32), fx)
 
 
+def test_parity_v6_slot_form(monkeypatch):
+    """The opt-in two-choice slot form of the IPv6 groups (INFW_V6_FORM=b2: two groups per 64-B bucket, cuckoo
+    placement, second-bucket reads behind the DISPLACED flag) classifies bit-identically — configs[2] (one-record
+    groups) and configs[4] (two-record groups taking a whole bucket, > 2 records in the Waldvogel table)."""
+    monkeypatch.setenv("INFW_V6_FORM", "b2")
+    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
+    assert_parity(r, "cfg2-v6-slots")
+    r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 0, 0)
+    assert_parity(r, "cfg4-v6-slots")
+
+
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""
