@@ -50,8 +50,12 @@ def main():
             shutil.copy(p, os.path.join(dst, os.path.basename(p)))
     out = {"tag": tag, "workload_key": key, "packets_per_launch": n, "kernels": {}}
     stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
+    # the profiled kernel: the classify instantiation launched most (a bench may run another one untimed, e.g. the
+    # packer path's classify_c that --fused checks its results against); PMC rows are filtered to it as well
+    cls = [r for r in stats if "classify" in r["Name"]]
+    main_name = max(cls, key=lambda r: int(r["Calls"]))["Name"] if cls else ""
     for r in stats:
-        if "classify" in r["Name"]:
+        if r["Name"] == main_name:
             out["kernels"][r["Name"][:80]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                               "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     pmc = collections.defaultdict(list)
@@ -60,7 +64,7 @@ def main():
         if not name.startswith("pmc") or not os.path.exists(p):
             continue
         for r in csv.DictReader(open(p)):
-            if "classify" in r["Kernel_Name"]:
+            if r["Kernel_Name"] == main_name:
                 pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {k: sum(v) / len(v) for k, v in pmc.items()}
     out["pmc_avg_per_launch"] = avg
