@@ -76,6 +76,7 @@ struct Variant {
     int pairing = 0;  // 1: compiled parts, entry line at ((list * 16 + part) * 8 + cls) * 64 (classes of one part adjacent)
     int adapt = 0;    // 1: per-(list, class) part count — the fewest of 1..16 parts of <= 20 segments each — inside
                       // the compiled 16-line region (lines past the count are never touched)
+    int cls_p = 0;    // 1: one part count per class (the fewest with <= 1/256 of its lines over 20 segments)
 };
 
 }  // namespace
@@ -133,7 +134,31 @@ int main(int argc, char **argv) {
                             {"dense_short", false, false, 0, 64, 64, 1}, {"cuckoo", false, false, 0, 64, 64, 0, 1},
                             {"list_minor", false, false, 0, 64, 64, 0, 0, 0, 2},
                             {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3},
-                            {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1}};
+                            {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1},
+                            {"clsP", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 1}};
+    // per-class part counts for clsP
+    int cls_plog[INFW_NCLS];
+    for (int c = 0; c < INFW_NCLS; c++) {
+        cls_plog[c] = 4;
+        for (int pp = 0; pp < 4; pp++) {
+            uint64_t lines = 0, over = 0;
+            for (uint32_t l = 0; l < h.n_lists; l++) {
+                const auto &st = seg_starts[(size_t)l * INFW_NCLS + c];
+                const uint32_t w = 65536u >> pp;
+                for (uint32_t q = 0; q < (1u << pp); q++) {
+                    uint32_t nseg = 1;
+                    for (uint32_t x : st) nseg += x > q * w && x < (q + 1) * w;
+                    lines++;
+                    over += nseg > INFW_DT_CLEAF_SEGS;
+                }
+            }
+            if (over * 256 <= lines) {
+                cls_plog[c] = pp;
+                break;
+            }
+        }
+        printf("{\"class\": %d, \"plog2\": %d}\n", c, cls_plog[c]);
+    }
     for (int Q : {4, 8, 16}) {  // how many (list, class, part) lines overflow 20 segments
         uint64_t parts = 0, over = 0;
         for (const auto &st : seg_starts)
@@ -418,6 +443,8 @@ int main(int argc, char **argv) {
                     }
                     if (pb < 4) tc[nt - 1].addr = 3 * kSpace + (ei * 16 + (val >> (16 - pb))) * 64;
                 }
+                if (t.dt_plog2 == 4 && V.cls_p && cls_plog[cls] < 4)
+                    tc[nt - 1].addr = 3 * kSpace + (ei * 16 + (val >> (16 - cls_plog[cls]))) * 64;
                 if (t.dt_plog2 && V.mini) {  // mini entry first; the 64-B line only for parts with more segments
                     const auto &st = seg_starts[ei];
                     const uint32_t q = val >> 12, lo = q << 12, hi = lo + 4096;
