@@ -287,7 +287,9 @@ int infw_pack_frames_c(infw_ctx *ctx, int dev, const struct infw_frame_batch *fr
 /* kernel builds infw_pack_header()'s tuple from each frame's bytes [10, 58)  */
 /* in LDS — the XDP program's own input, kernel.c:412-462 per frame).          */
 /* Identical results and counters to infw_pack_frames + infw_classify.        */
-/* Frames must be readable over [frame, frame + min(linear_len, 58)).          */
+/* Reads are whole 16-byte aligned blocks that hold a byte of                  */
+/* [frame + 10, frame + min(linear_len, 58)): no block outside a frame's own   */
+/* bytes' blocks is touched (the packer's rule, infw_pack_frames).             */
 int infw_classify_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
                          uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
 
