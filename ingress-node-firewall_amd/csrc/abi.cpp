@@ -271,6 +271,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.short_mode = h.short_mode;
     t.n_levels = (uint32_t)h.levels.size();
     t.dt_plog2 = h.dt_plog2;
+    t.dt_pl = static_cast<const uint32_t *>(e.buf[TB_DTPL]);
+    t.n_dt_pl = (uint32_t)h.dt_pl.size();
 }
 
 static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {

@@ -129,8 +129,8 @@ struct KeyCount {
     __device__ __forceinline__ uint32_t total() const { return (acc & 0xFFFFu) + (acc >> 16); }
 };
 __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
-                                              uint32_t list, int cls, uint32_t v, uint32_t plog2) {
-    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + infw_dt_slot(list, cls, v, plog2));
+                                              uint32_t list, int cls, uint32_t v, uint32_t plog2, uint32_t p) {
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + infw_dt_slot_p(list, cls, v, plog2, p));
     u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
     if (a[0] & INFW_DT_ROOT) {
         KeyCount g(v);
@@ -361,7 +361,7 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2>
+          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -388,6 +388,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
     __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
     __shared__ uint32_t s_fw[kF ? kBlock / 64 : 1][kF ? 16 * kFrameWinWords : 1];  // per-wave frame windows
+    // kPl: the per-list part-count words (T.n_dt_pl == INFW_DT_PL_LISTS) mirrored in LDS
+    __shared__ uint32_t s_pl[kPl ? INFW_DT_PL_LISTS : 1];
+    if (kPl)
+        for (uint32_t i = threadIdx.x; i < INFW_DT_PL_LISTS; i += kBlock) s_pl[i] = T.dt_pl[i];
     if (kB6)
         for (int i = threadIdx.x; i < (int)(2u << kB6Log); i += kBlock) s_b6[i] = u32x4{0u, 0u, 0u, 0u};
     for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) {
@@ -663,7 +667,13 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
         uint32_t result = 0;
         if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32) ^ lst;  // diagnostic 2: no first-match stage
-        else if (G == 0 && lst) result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2);
+        else if (G == 0 && lst) {
+            // the (list, class)'s own part count when the epoch has them (infw_tables.h), else the uniform one
+            uint32_t p = T.dt_plog2;
+            if (kPl) p = (s_pl[lst - 1] >> (3 * cls)) & 7u;
+            else if (T.n_dt_pl) p = (T.dt_pl[lst - 1] >> (3 * cls)) & 7u;
+            result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2, p);
+        }
         // ---- first match, one lane per rule, G packets in flight
         uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
         while (G > 0 && pending) {
@@ -769,14 +779,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false, int kV6 = 2>
+          bool kF = false, int kV6 = 2, bool kPl = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -794,7 +804,10 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form
+    // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form; with
+    // per-list part counts their LDS copy takes half the word cache (INFW_DT_ADAPT=0 at compile: none)
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
+        launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)
         launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)

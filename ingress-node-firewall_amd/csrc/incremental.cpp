@@ -297,6 +297,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     }
     const uint64_t n_lists_after = h.n_lists + new_vids.size();
     if (n_lists_after >= (1u << 25)) return full("more than 2^25-1 rule lists");
+    if (!h.dt_pl.empty() && n_lists_after > h.dt_pl.size()) return full("more lists than the part-count table holds");
     std::unordered_map<uint32_t, int64_t> ref_delta;  // existing lists only
     for (const Edit &e : edits) {
         if (e.was != PendingMap::kAbsent) ref_delta[inc.list_of_vid.at((uint32_t)e.was)]--;
@@ -325,7 +326,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         const size_t per_list = (size_t)INFW_NCLS << h.dt_plog2;
         if (h.dte.size() < (lid + 1) * per_list) h.dte.resize((lid + 1) * per_list, infw_dt_line{});
         int rc = compile_rule_list(m.pool.vals[vid].data(), h.rules, &h.desc[(size_t)lid * INFW_DESC_STRIDE],
-                                   &h.dte[lid * per_list], h.dtl, h.dt_plog2);
+                                   &h.dte[lid * per_list], h.dtl, h.dt_plog2, h.dt_pl.empty() ? nullptr : &h.dt_pl[lid]);
+        if (!h.dt_pl.empty()) mark(ranges, TB_DTPL, (uint64_t)lid * 4, 4);
         if (rc) {
             inc.valid = false;  // the image is no longer trustworthy: the next commit recompiles
             set_error("incremental commit: decision-table leaf pool exhausted");

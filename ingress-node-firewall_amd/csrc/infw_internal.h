@@ -118,6 +118,7 @@ struct HostTables {
     std::vector<uint64_t> rules;
     std::vector<infw_dt_line> dte, dtl;  // decision-table entry and leaf lines
     uint32_t dt_plog2 = 0;               // value-axis parts per (list, class): 1 << dt_plog2
+    std::vector<uint32_t> dt_pl;         // per-list part counts (INFW_DT_PL_LISTS words) or empty (infw_tables.h)
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -142,7 +143,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1
 // The device-resident buffers of one image, in upload order.
 enum TableBuf {
     TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
-    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_COUNT
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_COUNT
 };
 // Host bytes of buffer b (at least one element, like the upload).
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);
@@ -161,7 +162,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
 // the per-class first-match decision-table entry lines, INFW_NCLS << plog2 of
 // them (leaf lines appended to leaves).
 int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules, uint64_t desc_out[INFW_DESC_STRIDE],
-                      infw_dt_line *entry_out, std::vector<infw_dt_line> &leaves, uint32_t plog2);
+                      infw_dt_line *entry_out, std::vector<infw_dt_line> &leaves, uint32_t plog2, uint32_t *pl_out = nullptr);
 // First-match step function of one class list (records {lo16, hi16, result32} in
 // scan order): segment starts ascending from 0 and the result of each segment.
 void step_function(const std::vector<uint64_t> &recs, std::vector<uint32_t> &starts, std::vector<uint32_t> &res);

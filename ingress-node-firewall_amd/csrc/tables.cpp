@@ -475,14 +475,48 @@ static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
     return 4;
 }
 
+// Does every one of the 2^p parts of a step function fit one decision line (no root)?  Mirrors
+// emit_decision_lines' forms: a compact leaf holds 20 segments when all of the part's results have a code.
+static bool parts_fit_one_line(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, uint32_t p) {
+    const bool compact_ok = dt_compact_allowed();
+    const uint32_t span = 65536u >> p;
+    size_t j = 0;
+    for (uint32_t q = 0; q < (1u << p); q++) {
+        const uint32_t lo = q * span, hi = lo + span;
+        while (j + 1 < starts.size() && starts[j + 1] <= lo) j++;
+        uint32_t S = 1;
+        bool compact = compact_ok && infw_dt_result_code(res[j]) <= 0xFFu;
+        for (size_t k = j + 1; k < starts.size() && starts[k] < hi; k++) {
+            S++;
+            compact = compact && infw_dt_result_code(res[k]) <= 0xFFu;
+        }
+        if (S > (compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS)) return false;
+    }
+    return true;
+}
+
+// pl_out (per-list part counts, infw_tables.h): each class is cut into the fewest 2^p <= 2^plog2 parts that fit
+// one line each, written at the start of its 2^plog2-line region; *pl_out gets p in bits [3c, 3c + 3).
 int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
                       uint64_t desc_out[INFW_DESC_STRIDE], infw_dt_line *entry_out,
-                      std::vector<infw_dt_line> &leaves, uint32_t plog2) {
+                      std::vector<infw_dt_line> &leaves, uint32_t plog2, uint32_t *pl_out) {
     int rc = 0;
     std::vector<uint64_t> per[INFW_NCLS];
     class_records(val, per);
+    uint32_t pl = 0;
+    std::vector<uint32_t> st, rs;
     for (int c = 0; c < INFW_DESC_STRIDE; c++) {
-        if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], &entry_out[(size_t)c << plog2], leaves, plog2);
+        uint32_t p = plog2;
+        if (c < INFW_NCLS && pl_out) {
+            step_function(per[c], st, rs);
+            for (uint32_t q = 0; q < plog2; q++)
+                if (parts_fit_one_line(st, rs, q)) {
+                    p = q;
+                    break;
+                }
+            pl |= p << (3 * c);
+        }
+        if (c < INFW_NCLS && !rc) rc = build_decision_table(per[c], &entry_out[(size_t)c << plog2], leaves, p);
         if (c >= INFW_NCLS || per[c].empty()) {
             desc_out[c] = 0;
             continue;
@@ -491,6 +525,7 @@ int compile_rule_list(const uint8_t *val, std::vector<uint64_t> &rules,
         rules.insert(rules.end(), per[c].begin(), per[c].end());
         desc_out[c] = off | (uint64_t)per[c].size() << 32;
     }
+    if (pl_out) *pl_out = pl;
     return rc;
 }
 
@@ -667,12 +702,16 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         std::vector<int> rc_t(nt, 0);
         std::vector<std::pair<size_t, size_t>> range_t(nt);
         const size_t ents = (size_t)INFW_NCLS << out.dt_plog2;
+        // per-list part counts when the list count fits the kernel's LDS copy (INFW_DT_ADAPT=0 turns them off)
+        const char *ea = getenv("INFW_DT_ADAPT");
+        const bool adapt = out.dt_plog2 > 0 && out.n_lists <= INFW_DT_PL_LISTS && !(ea && atoi(ea) == 0);
+        out.dt_pl.assign(adapt ? INFW_DT_PL_LISTS : 0, 0u);
         parallel_chunks(out.n_lists, nt, [&](int t, size_t a, size_t b) {
             range_t[t] = {a, b};
             for (size_t lid = a; lid < b && !rc_t[t]; lid++)
                 rc_t[t] = compile_rule_list(m.pool.vals[vid_of_lid[lid]].data(), rules_t[t],
                                             &out.desc[lid * INFW_DESC_STRIDE], &out.dte[lid * ents], leaves_t[t],
-                                            out.dt_plog2);
+                                            out.dt_plog2, adapt ? &out.dt_pl[lid] : nullptr);
         });
         size_t rbase = 0, lbase = 0;
         for (int t = 0; t < nt && !dt_rc; t++) {
@@ -1135,6 +1174,7 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
     case TB_DTL: INFW_HB(dtl);
     case TB_LEVELS: INFW_HB(levels);
     case TB_WILD: INFW_HB(wild);
+    case TB_DTPL: INFW_HB(dt_pl);
     default:
         *p = nullptr;
         *bytes = 0;
@@ -1172,6 +1212,8 @@ infw_dev_tables HostTables::view() const {
     t.n_levels = (uint32_t)levels.size();
     t.levels = levels.data();
     t.dt_plog2 = dt_plog2;
+    t.dt_pl = dt_pl.data();
+    t.n_dt_pl = (uint32_t)dt_pl.size();
     return t;
 }
 
