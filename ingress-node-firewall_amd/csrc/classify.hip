@@ -940,7 +940,12 @@ extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_
             launch<512, 0, 0, false, 6, true, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
-    if (T->lean) launch<768, 0, 0, false, 6, false, false, 11, 9, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    // with per-list part counts their LDS copy replaces another half of the word cache (2 x 80 KiB per CU)
+    if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean)
+        launch<768, 0, 0, false, 6, false, false, 10, 9, true, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    else if (T->n_dt_pl == INFW_DT_PL_LISTS)
+        launch<768, 0, 0, false, 6, false, false, 10, 9, false, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    else if (T->lean) launch<768, 0, 0, false, 6, false, false, 11, 9, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     else launch<768, 0, 0, false, 6, false, false, 11, 9, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
