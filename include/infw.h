@@ -458,6 +458,9 @@ struct infw_table_info {
     uint64_t v6_slot_buckets;  /* != 0: IPv6 groups in the two-choice slot    */
                                /* form, this many 64-B buckets (else one group */
                                /* per bucket at <= 1/8 load)                   */
+    uint32_t short_mode;       /* <= /32 key space: 0 DIR-24-8, 1 compressed   */
+                               /* 16-8-8, 2 none, 3 range form (/16 chunks)    */
+    uint32_t dxr_lines;        /* range lines of the range form                */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
 #define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */

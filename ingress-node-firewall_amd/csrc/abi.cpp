@@ -260,7 +260,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.levels = static_cast<const uint8_t *>(e.buf[TB_LEVELS]);
     t.wild = static_cast<const uint32_t *>(e.buf[TB_WILD]);
     t.n_wild = h.n_wild;
-    t.lean = h.short_mode != INFW_SHORT_COMPRESSED && h.n_overflow_groups == 0 && h.n_wild == 0;
+    t.lean = (h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_NONE) && h.n_overflow_groups == 0 &&
+             h.n_wild == 0;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.if_mult = h.if_mult;
     t.if_shift = h.if_shift;
@@ -273,6 +274,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.dt_plog2 = h.dt_plog2;
     t.dt_pl = static_cast<const uint32_t *>(e.buf[TB_DTPL]);
     t.n_dt_pl = (uint32_t)h.dt_pl.size();
+    t.dxr_idx = static_cast<const uint32_t *>(e.buf[TB_DXRI]);
+    t.dxr_lines = static_cast<const infw_dt_line *>(e.buf[TB_DXRL]);
 }
 
 static int upload_epoch(const HostTables &h, int ordinal, std::shared_ptr<DeviceEpoch> &out) {
@@ -590,7 +593,8 @@ int infw_table_commit(infw_ctx *ctx) {
         mode = INFW_COMMIT_FULL;
         std::unique_ptr<HostTables> h(new HostTables());
         int smode = -1;
-        if (const char *e = getenv("INFW_SHORT_TABLE")) smode = strcmp(e, "compressed") == 0 ? 1 : strcmp(e, "dir24") == 0 ? 0 : -1;
+        if (const char *e = getenv("INFW_SHORT_TABLE"))
+            smode = strcmp(e, "compressed") == 0 ? 1 : strcmp(e, "dir24") == 0 ? 0 : strcmp(e, "dxr") == 0 ? 3 : -1;
         IncState inc;
         rc = compile_tables(ctx->map, *h, smode, 4ull << 30, &inc);
         if (rc) return rc;  // the previous epoch stays live
@@ -685,6 +689,8 @@ int infw_table_commit(infw_ctx *ctx) {
     in.n_v6_groups = h.n_buckets;
     in.n_v6_overflow = h.n_overflow_groups;
     in.v6_slot_buckets = h.b2n;
+    in.short_mode = h.short_mode;
+    in.dxr_lines = h.short_mode == INFW_SHORT_DXR ? (uint32_t)h.dxr_lines.size() : 0u;
     in.commit_mode = mode;
     in.dt_parts = 1u << h.dt_plog2;
     in.patch_bytes = patched;

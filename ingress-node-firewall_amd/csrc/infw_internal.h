@@ -119,6 +119,8 @@ struct HostTables {
     std::vector<infw_dt_line> dte, dtl;  // decision-table entry and leaf lines
     uint32_t dt_plog2 = 0;               // value-axis parts per (list, class): 1 << dt_plog2
     std::vector<uint32_t> dt_pl;         // per-list part counts (INFW_DT_PL_LISTS words) or empty (infw_tables.h)
+    std::vector<uint32_t> dxr_idx;       // short_mode INFW_SHORT_DXR: index words (infw_tables.h)
+    std::vector<infw_dt_line> dxr_lines; //   and range lines
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -143,7 +145,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1
 // The device-resident buffers of one image, in upload order.
 enum TableBuf {
     TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
-    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_COUNT
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_DXRI, TB_DXRL, TB_COUNT
 };
 // Host bytes of buffer b (at least one element, like the upload).
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);

@@ -177,8 +177,10 @@ struct infw_dev_tables {
     uint32_t lean;             // 1: no compressed short table, no overflowed IPv6 group, no partial-ifindex prefix —
                                // the kernel may launch without those code paths (fewer live registers)
     uint64_t b2n;              // != 0: btab holds the two-choice slot form with this many buckets
-    const uint32_t *dt_pl;     // n_dt_pl != 0: per-list part counts, 3 bits per class (see infw_dt_part_log2)
+    const uint32_t *dt_pl;     // n_dt_pl != 0: per-list part counts, 3 bits per class (see infw_dt_slot_p)
     uint32_t n_dt_pl;
+    const uint32_t *dxr_idx;   // short_mode INFW_SHORT_DXR: n_slots << 16 index words
+    const struct infw_dt_line *dxr_lines;
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -370,6 +372,14 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 #define INFW_SHORT_DIR24 0u
 #define INFW_SHORT_COMPRESSED 1u
 #define INFW_SHORT_NONE 2u        // DIR-24-8 build without any <= /32 entry
+#define INFW_SHORT_DXR 3u         // range form: per /16 chunk one answer or one line of <= 11 ranges
+// Range form of the short table (DXR-style): per (slot, address bits 0..15) an index word holding either the
+// chunk's single answer (INFW_DXR_DIRECT | list+1) or the index of a 64-B range line: the chunk's <= 11 runs at
+// /32 granularity as 10 u16 keys in w[0..4] (key j = start of run j+1 minus 1, pad 0xFFFF, so "key < v" <=>
+// "run j+1 starts at or below v") and the runs' answers in w[5..15].  A lookup is the index word (L2-resident:
+// 256 KiB per slot) and at most one line per chunk, where DIR-24-8 spreads a /16../23 prefix over up to 16 lines.
+#define INFW_DXR_DIRECT 0x80000000u
+#define INFW_DXR_RUNS 11u
 
 // DIR-24-8 word (8 B).  Bits 63..62:
 //   00  plain: list+1 of the whole /24 in bits 0..31;
@@ -527,6 +537,12 @@ INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uin
 template <class T>
 INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
     if (t.short_mode == INFW_SHORT_DIR24) return infw_dir24_lookup(t, slot, a32);
+    if (t.short_mode == INFW_SHORT_DXR) {
+        const uint32_t w = t.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
+        if (w & INFW_DXR_DIRECT) return w & ~INFW_DXR_DIRECT;
+        const uint32_t *l = t.dxr_lines[w].w;
+        return l[5 + infw_keys_below(l, 0, 5, a32 & 0xFFFFu)];
+    }
     return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }
 

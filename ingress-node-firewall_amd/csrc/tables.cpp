@@ -815,6 +815,11 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     });
     out.short_mode = short_mode_req >= 0 ? (uint32_t)short_mode_req
                      : ((uint64_t)out.n_slots << 27) <= dir24_budget ? INFW_SHORT_DIR24 : INFW_SHORT_COMPRESSED;
+    // the range form is derived from the DIR-24-8 build image (kept as well: incremental commits patch that)
+    bool dxr = out.short_mode == INFW_SHORT_DXR;
+    if (dxr) out.short_mode = INFW_SHORT_DIR24;
+    out.dxr_idx.clear();
+    out.dxr_lines.clear();
     const bool dir24 = out.short_mode == INFW_SHORT_DIR24;
     if (const char *e = getenv("INFW_D24_INLINE")) out.d24_inline = atoi(e) != 0;
     out.l16.assign(dir24 ? 1 : (size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
@@ -884,6 +889,42 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
                     }
                 }
                 out.tbl8.insert(out.tbl8.end(), t8.begin(), t8.end());
+                if (dxr) {  // the runs of every /16 chunk at /32 granularity; > INFW_DXR_RUNS anywhere: no range form
+                    if (out.dxr_idx.empty()) out.dxr_idx.assign((size_t)out.n_slots << 16, INFW_DXR_DIRECT);
+                    uint32_t rs[INFW_DXR_RUNS], rv[INFW_DXR_RUNS];
+                    for (uint32_t b = 0; b < 65536 && dxr; b++) {
+                        uint32_t nr = 0;
+                        auto push = [&](uint32_t start, uint32_t v) {
+                            if (nr && rv[nr - 1] == v) return true;
+                            if (nr == INFW_DXR_RUNS) return false;
+                            rs[nr] = start;
+                            rv[nr++] = v;
+                            return true;
+                        };
+                        for (uint32_t i = 0; i < 256 && dxr; i++) {
+                            const uint32_t w = t24[((size_t)b << 8) | i];
+                            if (w & INFW_TBL8_FLAG) {
+                                const uint32_t *g = &t8[(size_t)(w & ~INFW_TBL8_FLAG) << 8];
+                                for (uint32_t x = 0; x < 256 && dxr; x++) dxr = push(i << 8 | x, g[x]);
+                            } else {
+                                dxr = push(i << 8, w);
+                            }
+                        }
+                        if (!dxr) break;
+                        uint32_t &iw = out.dxr_idx[((size_t)slot << 16) | b];
+                        if (nr == 1) {
+                            iw = INFW_DXR_DIRECT | rv[0];
+                            continue;
+                        }
+                        infw_dt_line l;
+                        uint16_t key[10];
+                        for (uint32_t j = 0; j < 10; j++) key[j] = j + 1 < nr ? (uint16_t)(rs[j + 1] - 1) : (uint16_t)0xFFFF;
+                        for (uint32_t k = 0; k < 5; k++) l.w[k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
+                        for (uint32_t j = 0; j < INFW_DXR_RUNS; j++) l.w[5 + j] = j < nr ? rv[j] : 0u;
+                        iw = (uint32_t)out.dxr_lines.size();
+                        out.dxr_lines.push_back(l);
+                    }
+                }
                 si = sj;
                 continue;
             }
@@ -907,7 +948,16 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     if (out.tbl24.empty()) {  // no <= /32 entry on any interface: nothing to index
         out.tbl24.push_back(0);
         if (out.short_mode == INFW_SHORT_DIR24) out.short_mode = INFW_SHORT_NONE;
+        dxr = false;
     }
+    if (dxr && !out.dxr_idx.empty()) {
+        out.short_mode = INFW_SHORT_DXR;
+    } else {
+        out.dxr_idx.clear();
+        out.dxr_lines.clear();
+    }
+    if (out.dxr_idx.empty()) out.dxr_idx.push_back(INFW_DXR_DIRECT);
+    if (out.dxr_lines.empty()) out.dxr_lines.push_back(infw_dt_line{});
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
     if (out.nodes.empty()) out.nodes.push_back(infw_bnode{});
     if (out.vpool.empty()) out.vpool.push_back(0);
@@ -1175,6 +1225,8 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
     case TB_LEVELS: INFW_HB(levels);
     case TB_WILD: INFW_HB(wild);
     case TB_DTPL: INFW_HB(dt_pl);
+    case TB_DXRI: INFW_HB(dxr_idx);
+    case TB_DXRL: INFW_HB(dxr_lines);
     default:
         *p = nullptr;
         *bytes = 0;
@@ -1187,7 +1239,7 @@ infw_dev_tables HostTables::view() const {
     memset(&t, 0, sizeof(t));
     t.wild = wild.data();
     t.n_wild = n_wild;
-    t.lean = short_mode != INFW_SHORT_COMPRESSED && n_overflow_groups == 0 && n_wild == 0;
+    t.lean = (short_mode == INFW_SHORT_DIR24 || short_mode == INFW_SHORT_NONE) && n_overflow_groups == 0 && n_wild == 0;
     t.if_keys = if_keys.data();
     t.if_slot = if_slot.data();
     t.if_mask = (uint32_t)if_keys.size() - 1;
@@ -1214,6 +1266,8 @@ infw_dev_tables HostTables::view() const {
     t.dt_plog2 = dt_plog2;
     t.dt_pl = dt_pl.data();
     t.n_dt_pl = (uint32_t)dt_pl.size();
+    t.dxr_idx = dxr_idx.data();
+    t.dxr_lines = dxr_lines.data();
     return t;
 }
 

@@ -119,7 +119,8 @@ class TableInfo(C.Structure):
                 ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double),
                 ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64),
                 ("commit_mode", C.c_uint32), ("dt_parts", C.c_uint32), ("patch_bytes", C.c_uint64),
-                ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("v6_slot_buckets", C.c_uint64)]
+                ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("v6_slot_buckets", C.c_uint64),
+                ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12

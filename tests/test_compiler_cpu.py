@@ -33,6 +33,16 @@ def walk_vs_oracle(entries, tuples_from, n=20000, seed=1):
     return c, res
 
 
+@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG0_DEMO, 0, 0), (W.CFG1_V4_10K, 0, 0), (W.CFG2_MIXED_1M, 100000, 512),
+                                            (W.CFG4_ADVERSARIAL, 20000, 64)])
+def test_workloads_range_short_table(monkeypatch, cfg, npfx, ntmpl):
+    """The range form of the short table (INFW_SHORT_TABLE=dxr): the host walk equals the oracle."""
+    monkeypatch.setenv("INFW_SHORT_TABLE", "dxr")
+    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
+    c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
+    assert c.info()["short_mode"] == 3 and c.info()["dxr_lines"] > 0
+
+
 @pytest.mark.parametrize("cfg,npfx,ntmpl,v6_form", [(W.CFG0_DEMO, 0, 0, ""), (W.CFG1_V4_10K, 0, 0, ""),
                                                     (W.CFG2_MIXED_1M, 100000, 512, "std"),
                                                     (W.CFG2_MIXED_1M, 100000, 512, "b2"),

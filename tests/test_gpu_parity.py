@@ -330,6 +330,18 @@ def test_parity_v6_slot_form(monkeypatch):
     assert_parity(r, "cfg4-v6-slots")
 
 
+def test_parity_range_short_table(monkeypatch):
+    """The range form of the <= /32 key space (INFW_SHORT_TABLE=dxr: per /16 chunk one answer or one line of
+    <= 11 runs) classifies bit-identically on configs[1], [2] (100k prefixes) and [4]."""
+    monkeypatch.setenv("INFW_SHORT_TABLE", "dxr")
+    r = check_cfg(W.CFG1_V4_10K, 1 << 18)
+    assert_parity(r, "cfg1-dxr")
+    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
+    assert_parity(r, "cfg2-dxr")
+    r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64)
+    assert_parity(r, "cfg4-dxr")
+
+
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""
