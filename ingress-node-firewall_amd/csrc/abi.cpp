@@ -260,7 +260,8 @@ static void bind_view(DeviceEpoch &e, const HostTables &h) {
     t.levels = static_cast<const uint8_t *>(e.buf[TB_LEVELS]);
     t.wild = static_cast<const uint32_t *>(e.buf[TB_WILD]);
     t.n_wild = h.n_wild;
-    t.lean = (h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_NONE) && h.n_overflow_groups == 0 &&
+    t.lean = (h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_NONE ||
+              h.short_mode == INFW_SHORT_DXR) && h.n_overflow_groups == 0 &&
              h.n_wild == 0;
     t.if_mask = (uint32_t)h.if_keys.size() - 1;
     t.if_mult = h.if_mult;

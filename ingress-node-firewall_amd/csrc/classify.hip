@@ -55,7 +55,8 @@ template <bool kCache, int kLog, bool kLean = false>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                         unsigned long long *s_c24) {
     if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u)
-        return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(T, slot, a32) : 0u)
+        return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(T, slot, a32)
+                        : T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, slot, a32) : 0u)
                      : infw_short_lookup(T, slot, a32);
     const uint32_t key = slot << 24 | a32 >> 8;
     const uint32_t idx = (key * 0x9E3779B1u) >> (32 - kLog);
@@ -646,7 +647,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
                             s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
                     } else if (!v6 && !d24) {
-                        sh = kLean ? 0u : infw_short_lookup(T, (uint32_t)slot, a32);  // compressed / no short table
+                        // range form / compressed / no short table
+                        sh = kLean ? (T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, (uint32_t)slot, a32) : 0u)
+                                   : infw_short_lookup(T, (uint32_t)slot, a32);
                     }
                     if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log, kLean>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;

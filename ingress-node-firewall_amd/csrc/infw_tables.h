@@ -535,14 +535,17 @@ INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uin
 }
 
 template <class T>
+INFW_TD uint32_t infw_dxr_lookup(const T &t, uint32_t slot, uint32_t a32) {
+    const uint32_t w = t.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
+    if (w & INFW_DXR_DIRECT) return w & ~INFW_DXR_DIRECT;
+    const uint32_t *l = t.dxr_lines[w].w;
+    return l[5 + infw_keys_below(l, 0, 5, a32 & 0xFFFFu)];
+}
+
+template <class T>
 INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
     if (t.short_mode == INFW_SHORT_DIR24) return infw_dir24_lookup(t, slot, a32);
-    if (t.short_mode == INFW_SHORT_DXR) {
-        const uint32_t w = t.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
-        if (w & INFW_DXR_DIRECT) return w & ~INFW_DXR_DIRECT;
-        const uint32_t *l = t.dxr_lines[w].w;
-        return l[5 + infw_keys_below(l, 0, 5, a32 & 0xFFFFu)];
-    }
+    if (t.short_mode == INFW_SHORT_DXR) return infw_dxr_lookup(t, slot, a32);
     return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }
 

@@ -1239,7 +1239,7 @@ infw_dev_tables HostTables::view() const {
     memset(&t, 0, sizeof(t));
     t.wild = wild.data();
     t.n_wild = n_wild;
-    t.lean = (short_mode == INFW_SHORT_DIR24 || short_mode == INFW_SHORT_NONE) && n_overflow_groups == 0 && n_wild == 0;
+    t.lean = (short_mode == INFW_SHORT_DIR24 || short_mode == INFW_SHORT_NONE || short_mode == INFW_SHORT_DXR) && n_overflow_groups == 0 && n_wild == 0;
     t.if_keys = if_keys.data();
     t.if_slot = if_slot.data();
     t.if_mask = (uint32_t)if_keys.size() - 1;
