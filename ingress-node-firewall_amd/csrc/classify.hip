@@ -599,6 +599,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     const uint32_t key = (uint32_t)slot << 24 | a32 >> 8;
                     const uint32_t cidx = (key * 0x9E3779B1u) >> (32 - kC24Log);
                     bool need24 = !v6 && d24;
+                    const bool needx = !v6 && T.short_mode == INFW_SHORT_DXR;  // range form: index word in the round
+                    uint32_t wx = 0;
                     uint32_t sh = 0;
                     if (kCache && need24 && slot < 256) {
                         const unsigned long long e = s_c24[cidx];
@@ -628,6 +630,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         }
                     }
                     if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+                    if (needx) wx = T.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
                     if (need6) {
                         bi = b2 ? INFW_B2_INDEX(bhash >> 32, T.b2n) : bhash & T.bmask;
                         const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
@@ -646,6 +649,28 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         sh = d24_value(T, w24, a32);
                         if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
                             s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
+                    } else if (needx) {
+                        if (wx & INFW_DXR_DIRECT) {
+                            sh = wx & ~INFW_DXR_DIRECT;
+                        } else {
+                            const u32x4 *l = reinterpret_cast<const u32x4 *>(T.dxr_lines + wx);
+                            const u32x4 k0 = l[0], k1 = l[1], v2 = l[2], v3 = l[3];
+                            KeyCount kc(a32 & 0xFFFFu);
+                            kc.add(k0[0]); kc.add(k0[1]); kc.add(k0[2]); kc.add(k0[3]); kc.add(k1[0]);
+                            const uint32_t k = kc.total();  // answers in w[5..15]
+                            uint32_t r = k1[1];
+                            r = k >= 1 ? k1[2] : r;
+                            r = k >= 2 ? k1[3] : r;
+                            r = k >= 3 ? v2[0] : r;
+                            r = k >= 4 ? v2[1] : r;
+                            r = k >= 5 ? v2[2] : r;
+                            r = k >= 6 ? v2[3] : r;
+                            r = k >= 7 ? v3[0] : r;
+                            r = k >= 8 ? v3[1] : r;
+                            r = k >= 9 ? v3[2] : r;
+                            r = k >= 10 ? v3[3] : r;
+                            sh = r;
+                        }
                     } else if (!v6 && !d24) {
                         // range form / compressed / no short table
                         sh = kLean ? (T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, (uint32_t)slot, a32) : 0u)
