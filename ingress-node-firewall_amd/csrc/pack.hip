@@ -38,28 +38,22 @@ __global__ __launch_bounds__(256) void pack_frames_kernel(const infw_frame_batch
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
         const uint64_t wbase = base + 64u * wv;
-        // round r: chunk (lane & 3) of frame 16r + (lane >> 2); the four rounds' loads are all issued before any
-        // is stored (tools/micro/hdr.hip: 3.2 ms per 134M frames with them in flight together)
-        uint4 v[4];
-#pragma unroll
-        for (uint32_t r = 0; r < 4; r++) {
-            const uint64_t fi = wbase + 16 * r + (lane >> 2);
-            v[r] = make_uint4(0, 0, 0, 0);
+        for (uint32_t r = 0; r < 4; r++) {  // round r: chunk (lane & 3) of frame 16r + (lane >> 2)
+            const uint32_t j = 16 * r + (lane >> 2), c = lane & 3u;
+            const uint64_t fi = wbase + j;
+            uint4 v = make_uint4(0, 0, 0, 0);
             if (fi < n) {
                 const uint8_t *f = fb.frames + (fb.offsets ? fb.offsets[fi] : fi * fb.stride);
                 const uint32_t lin = fb.linear_len[fi];
-                const uintptr_t first = ((uintptr_t)f + kWinLo) & ~(uintptr_t)15, at = first + 16u * (lane & 3u);
+                const uintptr_t first = ((uintptr_t)f + kWinLo) & ~(uintptr_t)15, at = first + 16u * c;
                 if (lin > kWinLo && at < (uintptr_t)f + (lin < kWinHi ? lin : kWinHi))
-                    v[r] = *reinterpret_cast<const uint4 *>(at);
+                    v = *reinterpret_cast<const uint4 *>(at);
             }
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < 4; r++) {
-            uint32_t *d = ww + (16 * r + (lane >> 2)) * kWinWords + 4 * (lane & 3u);
-            d[0] = v[r].x;
-            d[1] = v[r].y;
-            d[2] = v[r].z;
-            d[3] = v[r].w;
+            uint32_t *d = ww + j * kWinWords + 4 * c;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
         }
         __syncthreads();
         const uint64_t i = wbase + lane;
