@@ -12,8 +12,8 @@ OBJ      := $(PKG)/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
 EXTRA    ?=
 
-LIB_SRCS := $(SRC)/abi.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp $(SRC)/classify.hip \
-            $(SRC)/pack.hip $(SRC)/patch.hip
+LIB_SRCS := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp \
+            $(SRC)/classify.hip $(SRC)/pack.hip $(SRC)/patch.hip
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 
@@ -22,6 +22,16 @@ all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so
 # classify.hip: the LDS counter atomics are issued by one lane or at per-lane addresses, where the atomic
 # optimizer's wave scan (mbcnt, ballot count, multiply) is pure overhead in the hot loop
 $(OBJ)/classify.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+
+# build id (infw_build_id()): a hash of the kernel / table-layout sources and the flags they are compiled with;
+# bench.py only attaches a profile's PMC figures to a line when the profile was taken on the same build id
+BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h
+$(OBJ)/infw_build_id.h: $(BUILDID_SRCS) Makefile
+	@mkdir -p $(OBJ)
+	@printf '#define INFW_BUILD_ID "%s"\n' "$$( (cat $(BUILDID_SRCS); echo '$(HIPFLAGS) $(EXTRA) $(ARCH)') | sha256sum | cut -c1-16)" > $@.tmp
+	@cmp -s $@.tmp $@ && rm -f $@.tmp || mv $@.tmp $@
+$(OBJ)/abi.cpp.o: $(OBJ)/infw_build_id.h
+$(OBJ)/abi.cpp.o: HIPFLAGS += -I$(OBJ)
 
 $(OBJ)/%.o: $(SRC)/% $(HDRS)
 	@mkdir -p $(OBJ)

@@ -5,14 +5,23 @@ One step = one pass of the hot path (parse -> LPM -> first-match scan ->
 per-rule stats) over one resident batch of synthetic SoA packets per GPU, plus
 (N > 1) the RCCL all-reduce of the 1024 x 4 u64 per-rule statistics.
 
-  python bench.py [--gpus N --steps K --warmup W]       (N > 1 under torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
 
-Rank 0 prints ONE JSON line.  Workload (N=1 and per GPU at N>1):
+Launch: with --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
+N rank processes itself (torch.multiprocessing spawn; the parent never touches
+the GPU) and they form an RCCL process group over 127.0.0.1.  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank and --gpus, when
+given, must equal WORLD_SIZE.  --spawn takes the spawn path at N = 1 too (an
+RCCL group of one).  Rank 0 prints ONE JSON line; `rccl_world_size` is the
+process group's size (null without one) and `per_rank` each rank's kernel time.
+
+Workload (N=1 and per GPU at N>1):
 BASELINE.json configs[2] — 1M mixed IPv4/IPv6 prefixes, BGP-like lengths,
 4 ifindexes, 4096 interned 99-rule lists, Zipf(1.1) traffic — with a
 128M-packet batch per GPU (configs[3]'s 1B-packet job is 8 x 128M).
 Packets are generated on the device from their global index, so a rank's
-shard is identical at any GPU count (weak scaling).
+shard is identical at any GPU count (weak scaling).  The table is compiled once
+(rank 0) and handed to the other ranks as an image (infw_table_export/import).
 
   --global-packets G   configs[3]'s fixed job: G packets in total, rank g of k
                        takes [g*G/k, (g+1)*G/k) (strong scaling); the line's
@@ -20,6 +29,11 @@ shard is identical at any GPU count (weak scaling).
                        counters of one step) is then identical for every k.
   --templates T        distinct rule lists (T >= prefixes: one 1200-B value per
                        key, configs[2]'s distinct-lists variant).
+  --host-walk          TEST ONLY (tests/test_bench_launch.py): no GPU; each rank
+                       walks its shard through the compiled host table image
+                       (infw_debug_walk) and the counters go through the same
+                       StatsExchange over gloo.  Checks the launcher, sharding
+                       and exchange; the line says it is not a measurement.
 """
 from __future__ import annotations
 
@@ -112,9 +126,16 @@ def workload_key(cfg, templates, prefixes):
     return f"cfg{cfg}" + ("_distinct" if templates and templates >= (prefixes or 1000000) else "")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node: > 1 spawns the ranks unless launched by torch.distributed.run, "
+                         "where it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--spawn", action="store_true", help="take the spawn path (own RCCL process group) at N = 1 too")
+    ap.add_argument("--host-walk", action="store_true",
+                    help="TEST ONLY: no GPU, ranks walk the compiled host image over gloo (not a measurement)")
+    ap.add_argument("--compile-per-rank", action="store_true",
+                    help="every rank compiles the table itself instead of importing rank 0's image")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 27, help="packets per GPU per step")
@@ -140,11 +161,187 @@ def parse():
     ap.add_argument("--fused", action="store_true",
                     help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
                          "no SoA batch written or read; checked untimed against the packer path's results")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def main(argv=None):
+    """Launcher.  Under torch.distributed.run (WORLD_SIZE set) this process is one rank.  Otherwise --gpus N > 1
+    (or --spawn) starts N rank processes with torch.multiprocessing's spawn start method: fresh interpreters, so
+    nothing of the parent's state — which never touches the GPU — is inherited, and each rank binds its own GPU."""
+    args = parse(argv)
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
+        return run_rank(args)
+    n = args.gpus or 1
+    if n > 1 or args.spawn:
+        return spawn_ranks(args, n)
+    return run_rank(args)
+
+
+def spawn_ranks(args, n):
+    import torch.multiprocessing as mp
+    if not args.host_walk:
+        import torch
+        have = torch.cuda.device_count()  # counts devices without initialising one (the parent never does)
+        if n > have:
+            sys.exit(f"bench.py: --gpus {n} but {have} HIP device(s) are visible")
+    mp.start_processes(_rank_entry, args=(args, n, free_port()), nprocs=n, start_method="spawn", join=True)
+
+
+def _rank_entry(i, args, n, port):
+    os.environ.update(RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run_rank(args)
+
+
+def share_tables(args, clf, wl, rank, world, use_dist, log):
+    """The rule table on this rank's context: compiled once by rank 0 and imported by the others
+    (infw_table_export -> a /dev/shm file -> infw_table_import: no other rank compiles), or compiled by every rank
+    with --compile-per-rank.  Returns (how, seconds)."""
+    import mmap
+    import torch.distributed as dist
+    t0 = time.time()
+    if not use_dist or world == 1 or args.compile_per_rank:
+        wl.load_into(clf)
+        clf.commit()
+        return "compiled", time.time() - t0
+    path = [None]
+    if rank == 0:
+        wl.load_into(clf)
+        clf.commit()
+        path[0] = f"/dev/shm/infw_bench_{os.getpid()}_{os.environ.get('MASTER_PORT', '0')}.img"
+        try:
+            size = clf.export_size()
+            with open(path[0], "w+b") as f:
+                f.truncate(size)
+                with mmap.mmap(f.fileno(), size) as mm:
+                    import ctypes as C
+                    buf = (C.c_char * size).from_buffer(mm)
+                    clf.export_into(C.addressof(buf), size)
+                    del buf
+        except OSError as e:  # no shared memory: every rank compiles
+            log(f"[bench] table image export failed ({e}); ranks compile their own tables")
+            path[0] = None
+    dist.broadcast_object_list(path, src=0)
+    how = "compiled"
+    if rank != 0:
+        if path[0] is None:
+            wl.load_into(clf)
+            clf.commit()
+        else:
+            import ctypes as C
+            with open(path[0], "rb") as f:
+                size = os.fstat(f.fileno()).st_size
+                # a private (copy-on-write) mapping: ctypes needs a writable buffer, and nothing writes it
+                with mmap.mmap(f.fileno(), size, access=mmap.ACCESS_COPY) as mm:
+                    buf = (C.c_char * size).from_buffer(mm)
+                    clf.import_image((C.addressof(buf), size))
+                    del buf
+            how = "imported"
+    dist.barrier()
+    if rank == 0 and path[0]:
+        os.unlink(path[0])
+    return how, time.time() - t0
+
+
+def gather_ranks(values, world, use_dist, dev=None):
+    """Every rank's `values` (a list of floats), in rank order."""
+    if not use_dist:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
+def host_counters(results, pkt_len):
+    """Per-rule counters implied by result words (kernel.c:441-456, :376-387) — the host walk's stand-in for the
+    kernel's device counters."""
+    import numpy as np
+    out = np.zeros((1024, 4), np.uint64)
+    act, key = results & 0xFF, (results >> 8) & 0xFFFF
+    for a, col in ((2, 0), (1, 2)):  # XDP_PASS allow, XDP_DROP deny
+        sel = (act == a) & (key < 1024)
+        np.add.at(out[:, col], key[sel], np.uint64(1))
+        np.add.at(out[:, col + 1], key[sel], pkt_len[sel].astype(np.uint64))
+    return out
+
+
+def run_host_walk(args, world, rank, use_dist, log):
+    """TEST ONLY (--host-walk): the launcher, sharding, table sharing and StatsExchange of run_rank on a CPU box —
+    gloo instead of RCCL, and each step's classification is infw_debug_walk over the compiled host image (the
+    kernel's lookup code run on the host), not the HIP kernel.  The JSON line says it is no measurement."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import infw
+    from infw import workloads as W
+    if use_dist:
+        dist.init_process_group("gloo")
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes or 20000, n_templates=args.templates or 64)
+    clf = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 16)
+    how, setup_s = share_tables(args, clf, wl, rank, world, use_dist, log)
+    if args.global_packets:
+        start, end = shard_range(args.global_packets, rank, world)
+        n = end - start
+    else:
+        n = min(args.batch, 1 << 16)
+        start = rank * n
+    tuples = wl.tuples(start, n) if n else np.zeros((0, 8), np.uint32)
+    ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64), use_dist)
+
+    def step(k):
+        buf = ex.begin(k)
+        if n:
+            buf.copy_(torch.from_numpy(host_counters(clf.debug_walk(tuples), tuples[:, 5]).view(np.int64)))
+        ex.end(k)
+
+    for k in range(args.warmup):
+        step(k)
+    ex.drain()
+    ex.total.zero_()
+    if use_dist:
+        dist.barrier()
+    ts = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    ex.drain()
+    if use_dist:
+        dist.barrier()
+    per_rank = gather_ranks([time.perf_counter() - ts, 0.0, setup_s, 1.0 if how == "imported" else 0.0, 0.0,
+                             float(n)], world, use_dist)
+    elapsed = max(r[0] for r in per_rank)
+    assert not bool((ex.total % max(args.steps, 1)).any()), "steps' counters differ"
+    digest = stats_digest((ex.total // max(args.steps, 1)).numpy())
+    job = args.global_packets if args.global_packets else n * world
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC + " [host-walk selftest: not a measurement]", "value": round(job * args.steps / elapsed / 1e6, 4),
+            "unit": "Mpps", "valid_measurement": False, "n_gpus": 0, "rccl_world_size": dist.get_world_size() if use_dist
+            else None, "backend": "gloo" if use_dist else None, "steps": args.steps, "warmup": args.warmup,
+            "scaling": "strong" if args.global_packets else "weak", "build_id": infw.build_id(),
+            "config": {"workload_key": workload_key(args.cfg, args.templates, args.prefixes), "prefixes": wl.n_entries,
+                       "global_batch": job, "packets_counted_in_stats": int(ex.total[:, 0].sum() + ex.total[:, 2].sum())
+                       // max(args.steps, 1), "stats_digest": digest},
+            "per_rank": [{"rank": r, "tables": "imported" if v[3] else "compiled", "packets_per_step": int(v[5])}
+                         for r, v in enumerate(per_rank)]}), flush=True)
+    if use_dist:
+        dist.destroy_process_group()
+
+
+def run_rank(args):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -156,32 +353,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_dist = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run (any N, 1 included)
+    use_dist = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run or spawned (any N, 1 included)
+
+    def log(*a):
+        if rank == 0:
+            print(*a, file=sys.stderr, flush=True)
+
+    if args.host_walk:
+        return run_host_walk(args, world, rank, use_dist, log)
     if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    def log(*a):
-        if rank == 0:
-            print(*a, file=sys.stderr, flush=True)
-
-    # ---- tables (host compile, replicated on every GPU)
-    t0 = time.time()
+    # ---- tables: compiled once (rank 0, imported by the other ranks), replicated on every GPU
     wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
     if args.uniform:
         wl.uniform_sources()
     clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16)
-    wl.load_into(clf)
-    t1 = time.time()
-    clf.commit()
-    commit_s = time.time() - t1
+    how, setup_s = share_tables(args, clf, wl, rank, world, use_dist, log)
+    commit_s = setup_s
     info = clf.info()
-    import resource
-    peak_rss_gib = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # ru_maxrss: KiB on Linux
-    log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries loaded in {t1 - t0:.1f}s, commit {commit_s:.1f}s "
-        f"(compile {info['compile_ms']:.0f} ms, upload {info['upload_ms']:.0f} ms, "
+    log(f"[bench] cfg{args.cfg}: {wl.n_entries} entries, tables {how} in {setup_s:.1f}s "
+        f"(compile/parse {info['compile_ms']:.0f} ms, upload {info['upload_ms']:.0f} ms, "
         f"{info['device_bytes'] / 2**20:.0f} MiB/GPU, lists={info['n_lists']}, levels={info['n_long_levels']})")
 
     # ---- resident input shard, generated on the device by global packet index
@@ -208,11 +403,11 @@ def main():
     if args.from_frames:  # one untimed pack prices the compact tuple by the batch's IPv6 share
         clf.pack_frames_c(frames, f_lin[:n], f_ifx[:n], batch_c, pkt_len=f_len[:n], stride=stride)
         n6 = int(((batch_c.meta[:n] & 0xFFFF) == 0x86DD).sum().item())
-        algo_bytes = 24 + 12 * n6 / n
+        algo_bytes = 24 + 12 * n6 / max(n, 1)
     elif args.layout == "compact":  # the packer's production layout (infw_pack_frames_c); converted untimed here
         batch_c = clf.compact(batch, dev=0)
         n6 = int(((batch.meta & 0xFFFF) == 0x86DD).sum().item())
-        algo_bytes = 24 + 12 * n6 / n
+        algo_bytes = 24 + 12 * n6 / max(n, 1)
     else:
         algo_bytes = ALGO_BYTES_PER_PKT
     results = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
@@ -229,7 +424,7 @@ def main():
             del ref
             clf.stats_reset()
         args.layout = "frames"
-        algo_bytes = 27 + 12 * n6 / n  # frame bytes kernel.c reads (11 B IPv4, 23 B IPv6) + 12 B lengths/ifindex + result
+        algo_bytes = 27 + 12 * n6 / max(n, 1)  # frame bytes kernel.c reads (11 B IPv4, 23 B IPv6) + 12 B lengths/ifindex + result
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -284,15 +479,16 @@ def main():
         kern_ms = [e[2].elapsed_time(e[1]) for e in evs]
     else:
         kern_ms = [e[0].elapsed_time(e[1]) for e in evs]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if use_dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    avg_kern_ms = sum(kern_ms) / len(kern_ms)
+    import resource
+    peak_rss_gib = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # ru_maxrss: KiB on Linux
+    mine = [elapsed, avg_kern_ms, setup_s, 1.0 if how == "imported" else 0.0, peak_rss_gib, float(n)]
+    per_rank = gather_ranks(mine, world, use_dist, dev)
+    elapsed = max(r[0] for r in per_rank)  # max over ranks
 
     job_pkts = args.global_packets if args.global_packets else n * world
     total_pkts = job_pkts * args.steps
     mpps = total_pkts / elapsed / 1e6
-    avg_kern_ms = sum(kern_ms) / len(kern_ms)
     achieved = algo_bytes * n / (avg_kern_ms * 1e-3) / 1e9
     total = ex.total
     counted = int(total[:, 0].sum().item() + total[:, 2].sum().item())
@@ -332,15 +528,18 @@ def main():
     extra = {}
     tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{wkey}.json")
     tj = json.load(open(tpath)) if os.path.exists(tpath) else None
-    if tj is not None and (tj.get("kernel") != kernel or tj.get("layout", "standard") != args.layout):
-        log(f"[bench] {tpath} was profiled on {tj.get('kernel')!r} ({tj.get('layout', 'standard')}), not "
-            f"{kernel!r} ({args.layout}): traffic figures omitted")
+    build_id = infw.build_id()
+    if tj is not None and (tj.get("build_id") != build_id or tj.get("kernel") != kernel or
+                           tj.get("layout", "standard") != args.layout):
+        log(f"[bench] {tpath} was profiled on build {tj.get('build_id')} {tj.get('kernel')!r} "
+            f"({tj.get('layout', 'standard')}), not build {build_id} {kernel!r} ({args.layout}): traffic figures omitted")
         tj = None
     if tj is not None:
         try:
             traffic = tj.get("hbm_bytes_per_packet", None)
             traffic = None if traffic is None else round(traffic * n)
-            traffic_from = f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {wkey})"
+            traffic_from = (f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {wkey}, "
+                            f"build {tj.get('build_id')})")
             # random-line model: the kernel's PMC L2 hits/misses per packet priced at the
             # chip's measured random-lookup rates; frac = that bound / the measured kernel time
             r = tj.get("line_rates")
@@ -367,6 +566,8 @@ def main():
         "value": round(mpps, 2),
         "unit": "Mpps",
         "n_gpus": world,
+        "rccl_world_size": dist.get_world_size() if use_dist else None,
+        "build_id": build_id,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -392,11 +593,17 @@ def main():
             "packets_counted_in_stats": counted,
             "stats_digest": digest,
             "tables": {"device_bytes_per_image": info["device_bytes"], "images_per_gpu": 2,
-                       "dt_parts": info["dt_parts"], "commit_s": round(commit_s, 2),
+                       "dt_parts": info["dt_parts"], "setup_s": round(commit_s, 2), "rank0": how,
                        "compile_ms": round(info["compile_ms"], 1), "upload_ms": round(info["upload_ms"], 1),
-                       # peak host RSS of this rank (table compile + workload): N ranks compile side by side
+                       # peak host RSS of rank 0 (table compile + workload); the others import its image
                        "host_peak_rss_gib": round(peak_rss_gib, 2)},
         },
+        # every rank: its own wall time of the K steps, average kernel time (HIP events on its launch stream),
+        # table setup and whether it compiled or imported rank 0's image, peak host RSS, packets per step
+        "per_rank": [{"rank": r, "elapsed_s": round(v[0], 5), "kernel_ms_avg": round(v[1], 4),
+                      "tables_setup_s": round(v[2], 2), "tables": "imported" if v[3] else "compiled",
+                      "host_peak_rss_gib": round(v[4], 2), "packets_per_step": int(v[5])}
+                     for r, v in enumerate(per_rank)],
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),

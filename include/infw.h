@@ -461,6 +461,13 @@ struct infw_table_info {
     uint32_t short_mode;       /* <= /32 key space: 0 DIR-24-8, 1 compressed   */
                                /* 16-8-8, 2 none, 3 range form (/16 chunks)    */
     uint32_t dxr_lines;        /* range lines of the range form                */
+    /* ABI 3: commit timing per device slot (the slots upload / patch in        */
+    /* parallel, one host thread each) and room to grow without another break.  */
+    double device_ms_max;      /* slowest slot's upload / patch of the last     */
+                               /* commit (wall, host thread of that slot)      */
+    uint32_t n_device_slots;   /* slots the last commit published to            */
+    uint32_t imported;         /* 1: the epoch came from infw_table_import      */
+    uint64_t reserved[14];     /* zero; future fields come out of this         */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
 #define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */
@@ -475,9 +482,34 @@ int infw_table_info(infw_ctx *ctx, struct infw_table_info *info);
 int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t *out);
 /* Last error string of this thread (static storage).                          */
 const char *infw_last_error(void);
-/* ABI version (bumped on incompatible change).                                */
-#define INFW_ABI_VERSION 2
+/* ABI version (bumped on incompatible change).  3: struct infw_table_info     */
+/* grew (and now ends in reserved space), infw_build_id, table export/import. */
+#define INFW_ABI_VERSION 3
 int infw_abi_version(void);
+/* Identity of the code this library was built from: a hash of the kernel and */
+/* table-layout sources and the flags they were compiled with (Makefile).       */
+/* Profiles taken on one build are only valid for the same build id.           */
+const char *infw_build_id(void);
+
+/* ------------------------------------------------------------------------ */
+/* Compiled-epoch images: compile once, install on many contexts.  The        */
+/* reference has one daemon per node driving one map (ebpfsyncer.go:70-125);  */
+/* here one process per GPU each holds a context, and instead of every rank    */
+/* compiling the same 1M-entry set, one exports its committed epoch (the      */
+/* entry set, the compiled host tables and the incremental-commit state) and  */
+/* the others import it.                                                       */
+/* ------------------------------------------------------------------------ */
+/* Serialise the last committed epoch.  buf == NULL: *size = bytes needed.     */
+/* -EBUSY when the pending set has uncommitted edits, -ENOSPC when cap is too  */
+/* small (*size says how much is needed).                                      */
+int infw_table_export(infw_ctx *ctx, void *buf, uint64_t cap, uint64_t *size);
+/* Install an exported epoch into a context whose map is empty: the entries    */
+/* become the committed set (get_next_key / lookup / later incremental commits */
+/* work as after a commit) and every device slot gets the image — no compile.  */
+/* -EBUSY: the context already holds entries or edits; -EINVAL: not an image  */
+/* of this library build (infw_build_id) or truncated; -ENOSPC: more entries   */
+/* than max_entries.                                                           */
+int infw_table_import(infw_ctx *ctx, const void *buf, uint64_t size);
 
 #ifdef __cplusplus
 }

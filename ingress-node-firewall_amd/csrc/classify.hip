@@ -510,7 +510,11 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 dst[1] = ch[r][1];
                 dst[2] = ch[r][2];
                 dst[3] = ch[r][3];
+                // the owners read other lanes' LDS writes: a wave-scope release/acquire pair orders them (the
+                // wave barrier alone is no memory fence to the compiler)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if ((lane >> 4) == (uint32_t)r) {  // the round's 16 owners read their frames' fields
                     const uint32_t e = frame_word(w, d, 12, cap);
                     et = cap >= 14u ? (e & 0xFFu) << 8 | ((e >> 8) & 0xFFu) : 0u;
@@ -525,7 +529,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         s3 = frame_word(w, d, 34, cap);
                     }
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();  // the next round rewrites the buffer
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             meta = et | proto << 16 | (cap > 255u ? 255u : cap) << 24;
             l4w = l4;

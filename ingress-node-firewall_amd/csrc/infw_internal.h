@@ -40,6 +40,12 @@ struct NodeVal {
     uint32_t vid;  // interned value id
 };
 
+// The entry set of a table image (image.cpp): interned values (1200 B each, in id order) and the nodes.
+struct ImageEntries {
+    std::vector<uint8_t> vals;
+    std::vector<std::pair<NodeKey, NodeVal>> nodes;
+};
+
 struct ValuePool {
     std::deque<std::array<uint8_t, 1200>> vals;  // deque: growing never copies the values held
     std::unordered_multimap<uint64_t, uint32_t> index;
@@ -81,6 +87,9 @@ struct PendingMap {
     PendingMap &operator=(const PendingMap &) = delete;
 
     int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
+    // An imported committed set into an empty map (image.cpp); clear() empties the map.
+    int install_committed(const ImageEntries &ent, std::string *why);
+    void clear();
     int remove(const lpm_ip_key_st *key);
     int lookup(const lpm_ip_key_st *key, uint8_t *val) const;
     int next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const;
@@ -153,6 +162,12 @@ struct DirtyRange {
     uint32_t buf;
     uint64_t off, len;  // bytes
 };
+// Table images (image.cpp): size, serialise, parse (nothing installed; ent/h/inc filled).
+uint64_t image_bytes(const PendingMap &m, const HostTables &h, const IncState &inc, const char *build_id);
+void image_write(const PendingMap &m, const HostTables &h, const IncState &inc, const char *build_id, uint8_t *out);
+int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEntries &ent, HostTables &h,
+               IncState &inc, std::string *why);
+
 // Apply m.dirty to the compiled image in place (DIR-24-8 words and tbl8 groups,
 // IPv6 buckets, appended rule lists), recording every byte range it changes.
 // Returns 0 when patched, 1 when the edit needs a full compile (*why says why;

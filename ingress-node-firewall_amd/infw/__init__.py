@@ -5,7 +5,7 @@ Package layout (ingress-node-firewall_amd/):
   lib/      libinfw.so (product) and libinfw_workload.so (bench/test workloads), built in-tree
   infw/     this Python mirror of the reference's pkg/ebpf + pkg/metrics API over the C ABI
 """
-from ._native import (BPF_ANY, BPF_EXIST, BPF_NOEXIST, COMMIT_FULL, COMMIT_INCREMENTAL, COMMIT_REUPLOAD,
+from ._native import (build_id, BPF_ANY, BPF_EXIST, BPF_NOEXIST, COMMIT_FULL, COMMIT_INCREMENTAL, COMMIT_REUPLOAD,
                       F_FULL_COMMIT, F_HOST_ONLY, F_KEEP_HOST_IMAGE, LIB_PATH, MAX_TARGETS,
                       XDP_DROP, XDP_PASS, InfwError, LpmIpKeySt, RuleStatisticsSt, RulesValSt, RuleTypeSt)
 from .core import Classifier, HostSoa, build_ebpf_key, key_from_fields, verdicts_from_results
@@ -16,5 +16,5 @@ __all__ = [
     "Classifier", "HostSoa", "build_ebpf_key", "key_from_fields", "verdicts_from_results", "IngNodeFwController",
     "IngressNodeFirewallRules", "ProtocolRule", "Statistics", "make_rules_val", "LpmIpKeySt", "RulesValSt",
     "RuleTypeSt", "RuleStatisticsSt", "InfwError", "BPF_ANY", "BPF_NOEXIST", "BPF_EXIST", "F_HOST_ONLY",
-    "F_KEEP_HOST_IMAGE", "F_FULL_COMMIT", "COMMIT_FULL", "COMMIT_INCREMENTAL", "COMMIT_REUPLOAD", "XDP_DROP", "XDP_PASS", "MAX_TARGETS", "LIB_PATH",
+    "build_id", "F_KEEP_HOST_IMAGE", "F_FULL_COMMIT", "COMMIT_FULL", "COMMIT_INCREMENTAL", "COMMIT_REUPLOAD", "XDP_DROP", "XDP_PASS", "MAX_TARGETS", "LIB_PATH",
 ]

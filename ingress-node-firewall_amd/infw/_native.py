@@ -120,7 +120,9 @@ class TableInfo(C.Structure):
                 ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64),
                 ("commit_mode", C.c_uint32), ("dt_parts", C.c_uint32), ("patch_bytes", C.c_uint64),
                 ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("v6_slot_buckets", C.c_uint64),
-                ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32)]
+                ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32),
+                ("device_ms_max", C.c_double), ("n_device_slots", C.c_uint32), ("imported", C.c_uint32),
+                ("reserved", C.c_uint64 * 14)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12
@@ -138,8 +140,9 @@ ABI_SYMBOLS = [
     "infw_debug_lookup_set", "infw_debug_keys_read", "infw_debug_keys_clear", "infw_classify_host",
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c", "infw_classify_frames",
     "infw_classify_frames_ex",
-    "infw_get_launch", "infw_events_capture",
+    "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
 ]
+ABI_VERSION = 3  # include/infw.h INFW_ABI_VERSION
 
 
 # torch (device memory, streams, RCCL) ships its own libamdhip64.so.7; loading it
@@ -209,6 +212,9 @@ _sig = {
     "infw_debug_keys_clear": (C.c_int, [C.c_void_p]),
     "infw_last_error": (C.c_char_p, []),
     "infw_abi_version": (C.c_int, []),
+    "infw_build_id": (C.c_char_p, []),
+    "infw_table_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "infw_table_import": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -275,3 +281,10 @@ for _name, (_res, _args) in _wsig.items():
     _f.argtypes = _args
 
 assert C.sizeof(EventHdrSt) == 8 and C.sizeof(EventRec) == 24
+if lib.infw_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH}: ABI {lib.infw_abi_version()}, these bindings are ABI {ABI_VERSION}: rebuild (make)")
+
+
+def build_id() -> str:
+    """infw_build_id(): hash of the kernel / table-layout sources and flags this library was built from."""
+    return lib.infw_build_id().decode()

@@ -99,12 +99,18 @@ class IngNodeFwController:
         desired = [LpmIpKeySt.from_buffer_copy(k) for k in key_to_rules]
         stale = self.get_stale_keys(desired)
         errs = self.purge_keys(stale)                        # errors logged, not fatal (loader.go:183-186)
+        # an update error (e.g. ENOSPC) ends the load (loader.go:187-188), but the reference's per-key map
+        # updates made before it are live: publish them rather than leave them pending for a later commit.
+        # The caller sees the update's own error; a commit failure after it is chained as its cause.
         try:
-            # an update error (e.g. ENOSPC) ends the load (loader.go:187-188), but the reference's per-key map
-            # updates made before it are live: publish them rather than leave them pending for a later commit
             self.add_or_update_rules(key_to_rules)
-        finally:
-            self.c.commit()                                  # publish as one epoch
+        except Exception as update_err:
+            try:
+                self.c.commit()
+            except Exception as commit_err:
+                raise update_err from commit_err
+            raise
+        self.c.commit()                                      # publish as one epoch
         return errs
 
     def get_stale_keys(self, desired: List[LpmIpKeySt]) -> List[LpmIpKeySt]:

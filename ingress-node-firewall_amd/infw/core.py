@@ -131,10 +131,38 @@ class Classifier:
     def commit(self) -> None:
         check(N.lib.infw_table_commit(self._ctx), "commit")
 
+    def export_size(self) -> int:
+        """Bytes of the committed epoch's image (infw_table_export with no buffer)."""
+        n = C.c_uint64(0)
+        check(N.lib.infw_table_export(self._ctx, None, 0, C.byref(n)), "table_export")
+        return n.value
+
+    def export_into(self, ptr: int, cap: int) -> int:
+        """infw_table_export into caller memory at `ptr` (e.g. a shared mmap); returns the image size."""
+        n = C.c_uint64(0)
+        check(N.lib.infw_table_export(self._ctx, ptr, cap, C.byref(n)), "table_export")
+        return n.value
+
+    def export_image(self) -> bytes:
+        """The committed epoch as an image another context (another rank's) can import."""
+        buf = C.create_string_buffer(self.export_size())
+        n = self.export_into(C.addressof(buf), len(buf))
+        return buf.raw[:n]
+
+    def import_image(self, image) -> None:
+        """infw_table_import: install an exported epoch (bytes, or (ptr, size) of caller memory) on an empty
+        context — its entries become the committed set and every device slot gets the tables, no compile."""
+        if isinstance(image, tuple):
+            ptr, size = image
+            check(N.lib.infw_table_import(self._ctx, ptr, size), "table_import")
+        else:
+            b = bytes(image)
+            check(N.lib.infw_table_import(self._ctx, b, len(b)), "table_import")
+
     def info(self) -> Dict[str, float]:
         ti = N.TableInfo()
         check(N.lib.infw_table_info(self._ctx, C.byref(ti)), "info")
-        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f != "pad0"}
+        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f not in ("pad0", "reserved")}
         d["full_reason"] = ti.full_reason.decode()
         return d
 

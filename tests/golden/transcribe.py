@@ -174,3 +174,187 @@ probes = [
 json.dump({"source": "SURVEY.md [probe] observations of the reference XDP object under BPF_PROG_TEST_RUN, restated; "
            "cases marked derived follow from the cited source lines", "frame_len_default": 0,
            "cases": probes}, open("survey_probes.json", "w"), indent=1)
+
+# --- test/e2e/functional/tests/e2e.go:176-831: the reference's behavioural table.  Each entry's INF objects are
+# generated the way the harness does it (e2e.go:879-945: source CIDRs = each pod's IP /32 and /128, rule orders
+# from nextSourceCIDRsOrder), merged into the node's InterfaceIngressRules as the operator does
+# (controllers/ingressnodefirewall_controller.go:329-347 mergeRuleSet :371-405, mergeFirewallProtocolRules
+# :409-425), and the expected connectivity comes from the entry's `reachables` (connectivity false after the
+# policy, e2e.go:971-975; true before it, :872-876), per protocol and family as reachabilityCheck (:1535-1621)
+# checks it: IPv4 for every protocol but ICMPv6, IPv6 (dual stack) for every protocol but ICMP, ICMP echo
+# requests type 8 / 128 code 0, transport connections to the reachable's port.  The deny events each blocked
+# connection must produce are GetTransportTestEvent / GetICMPTestEvent (test/e2e/events/events.go), matched by the
+# reference's own syslog regular expressions (events.go extractEventsFromString), copied here as data.
+# Assumptions, stated: a dual-stack cluster with ENABLE_SCTP=true (e2e.go:111-116, :158-164); the pod IPs, the
+# node interface's ifindex and the ephemeral source ports are synthetic (the cluster assigns them at run time).
+POD_IPS = {  # synthetic pod IPs (KinD's default dual-stack pod CIDRs 10.244.0.0/16, fd00:10:244::/56)
+    "e2e-inf-client-one": ("10.244.1.11", "fd00:10:244:1::b"), "e2e-inf-client-two": ("10.244.1.12", "fd00:10:244:1::c"),
+    "e2e-inf-client-three": ("10.244.1.13", "fd00:10:244:1::d"), "e2e-inf-client-four": ("10.244.1.14", "fd00:10:244:1::e"),
+    "e2e-inf-server-one": ("10.244.2.21", "fd00:10:244:2::15"), "e2e-inf-server-two": ("10.244.2.22", "fd00:10:244:2::16"),
+}
+C1, C2, C3, C4 = "e2e-inf-client-one", "e2e-inf-client-two", "e2e-inf-client-three", "e2e-inf-client-four"
+S1, S2 = "e2e-inf-server-one", "e2e-inf-server-two"
+SERVER_ONE_PORT, ALLOWED_PORT, SERVER_TWO_PORT, SERVER_ONE_RANGE = "80", "40000", "8080", "79-81"  # e2e.go:137-140
+TRANSPORT = ["TCP", "UDP", "SCTP"]     # e2e.go:154, :158-160 (SCTP with ENABLE_SCTP)
+ICMPS = ["ICMP", "ICMPv6"]             # e2e.go:155, :162-164 (ICMPv6 when not single stack)
+
+
+def block_port(port):                  # infwutils.GetTransportProtocolBlockPortRule (ingress-node-firewall.go:208-219)
+    return lambda proto, order: {"order": order, "protocol": proto, "ports": port, "action": "Deny"}
+
+
+def block_echo(proto, order):          # the e2e entries' ICMP closures + GetICMPBlockRule (:221-250)
+    return {"order": order, "protocol": proto, "icmp_type": 8 if proto == "ICMP" else 128, "icmp_code": 0,
+            "action": "Deny"}
+
+
+def block_port_or_echo(port):          # e2e.go:448-462: transport -> block port, ICMP -> block echo request
+    return lambda proto, order: (block_port(port)(proto, order) if proto in TRANSPORT else block_echo(proto, order))
+
+
+E2E = [  # (it, e2e.go line, testINFs [(interfaces, [(pods, protoRules)])], reachables [(src, dst, port)], protocols)
+    ("block a port with a single rule defining the destinations port", 191,
+     [(["eth0"], [([C1], [block_port(SERVER_ONE_PORT)])])], [(C1, S1, SERVER_ONE_PORT)], TRANSPORT),
+    ("block a port using a range when multiple source CIDRs exist", 228,
+     [(["eth0"], [([C1, C2], [block_port(SERVER_ONE_RANGE)])])], [(C1, S1, SERVER_ONE_PORT), (C2, S1, SERVER_ONE_PORT)],
+     TRANSPORT),
+    ("block multiple ports", 275,
+     [(["eth0"], [([C1], [block_port(SERVER_ONE_PORT), block_port(SERVER_TWO_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT), (C1, S2, SERVER_TWO_PORT)], TRANSPORT),
+    ("block port when rules for a source CIDR are located in multiple IngressNodeFirewall objects", 325,
+     [(["eth0"], [([C1], [block_port(ALLOWED_PORT)])]), (["eth0"], [([C1], [block_port(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT)], TRANSPORT),
+    ("merges transport protocol rules when source CIDRs overlap in multiple IngressNodeFirewalls and the count of "
+     "source CIDRs for each policy is different", 375,
+     [(["eth0"], [([C1], [block_port(ALLOWED_PORT)])]), (["eth0"], [([C1, C2], [block_port(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT), (C2, S1, SERVER_ONE_PORT)], TRANSPORT),
+    ("merges multiple IngressNodeFirewalls which contain multiple ingress entries with protocol rules for all "
+     "protocols", 440,
+     [(["eth0"], [([C1], [block_port_or_echo(SERVER_ONE_PORT)]), ([C2], [block_port_or_echo(SERVER_ONE_PORT)])]),
+      (["eth0"], [([C3], [block_port_or_echo(SERVER_ONE_PORT)]), ([C4], [block_port_or_echo(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT), (C2, S1, SERVER_ONE_PORT), (C3, S1, SERVER_ONE_PORT), (C4, S1, SERVER_ONE_PORT)],
+     TRANSPORT + ICMPS),
+    ("block port when rules for a source CIDR are located in multiple IngressNodeFirewall objects (2)", 585,
+     [(["eth0"], [([C1], [block_port(ALLOWED_PORT)])]), (["eth0"], [([C1], [block_port(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT)], TRANSPORT),
+    ("merges transport protocol rules when source CIDRs overlap in multiple IngressNodeFirewalls but the number of "
+     "source CIDRs in each policy is different", 635,
+     [(["eth0"], [([C1], [block_port(ALLOWED_PORT)])]), (["eth0"], [([C1, C2], [block_port(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT), (C2, S1, SERVER_ONE_PORT)], TRANSPORT),
+    ("block ICMP echo request", 697, [(["eth0"], [([C1], [block_echo])])], [(C1, S1, SERVER_ONE_PORT)], ICMPS),
+    ("non existent interface name doesn't block application of IngressNodeFirewall policy for valid interface", 744,
+     [(["doesntexist", "eth0"], [([C1], [block_port(SERVER_ONE_PORT)])])], [(C1, S1, SERVER_ONE_PORT)], ["TCP"]),
+    ("non existent interface name in unrelated IngressNodeFirewall doesn't block application of new "
+     "IngressNodeFirewalls policies", 781,
+     [(["doesntexist"], [([C1], [block_port(ALLOWED_PORT)])]), (["eth0"], [([C1], [block_port(SERVER_ONE_PORT)])])],
+     [(C1, S1, SERVER_ONE_PORT)], ["TCP"]),
+]
+
+
+def harness_infs(test_infs, protocols):
+    """e2e.go:879-945: INF objects from the templates; orders continue per source CIDR across objects."""
+    next_order = {}
+    infs = []
+    for interfaces, test_rules in test_infs:
+        ingress = []
+        for pods, proto_fns in test_rules:
+            cidrs = []
+            for pod in pods:
+                for ip, bits in ((POD_IPS[pod][0], 32), (POD_IPS[pod][1], 128)):   # v4SubnetLen / v6SubnetLen
+                    c = f"{ip}/{bits}"           # already canonical, so net.ParseCIDR's cidr.String() is the same text
+                    next_order.setdefault(c, 1)
+                    cidrs.append(c)
+            order = max([0] + [next_order[c] for c in cidrs])
+            rules = []
+            for proto in protocols:
+                for fn in proto_fns:
+                    rules.append(fn(proto, order))
+                    order += 1
+            for c in cidrs:
+                next_order[c] = order
+            ingress.append({"source_cidrs": cidrs, "rules": rules})
+        infs.append({"interfaces": interfaces, "ingress": ingress})
+    return infs
+
+
+def merge_rule_set(a, b):
+    """mergeRuleSet (controllers/ingressnodefirewall_controller.go:371-405) + mergeFirewallProtocolRules (:409-425)."""
+    for rb in b:
+        for cidr in rb["source_cidrs"]:
+            for ra in a:
+                if ra["source_cidrs"][0] == cidr:
+                    orders = [r["order"] for r in ra["rules"]]
+                    for r in rb["rules"]:
+                        assert r["order"] not in orders, "duplicate order: the operator reports a sync error"
+                        orders.append(r["order"])
+                    ra["rules"] = ra["rules"] + rb["rules"]
+                    break
+            else:
+                a.append({"source_cidrs": [cidr], "rules": list(rb["rules"])})
+    return a
+
+
+def node_state(infs):
+    """buildNodeStates (:267-350) for one node: every INF's ingress merged per interface, in object order."""
+    st = {}
+    for inf in infs:
+        for iface in inf["interfaces"]:
+            st[iface] = merge_rule_set(st.setdefault(iface, []), inf["ingress"])
+    return st
+
+
+def connections(reachables, protocols):
+    """reachabilityCheck (e2e.go:1535-1621): the packets one check sends, with the drop event it expects."""
+    out = []
+    for src, dst, port in reachables:
+        for proto in protocols:
+            for fam in (4, 6):
+                if (fam == 4 and proto == "ICMPv6") or (fam == 6 and proto == "ICMP"):
+                    continue
+                s, d = POD_IPS[src][fam == 6], POD_IPS[dst][fam == 6]
+                c = {"src": s, "dst": d, "family": fam, "protocol": proto, "interface": "eth0",
+                     "event": {"InterfaceName": "eth0", "SourceAddress": s, "DestinationAddress": d, "Action": "Deny",
+                               "Protocol": proto}}
+                if proto in TRANSPORT:
+                    c["dport"] = int(port)
+                    c["event"].update(DestinationPort=port, IcmpType=0, IcmpCode=0)
+                else:  # GetICMPTestEvent(proto, inf, src, dst, 0, 8 | 128): icmpCode 0, icmpType 8 / 128
+                    c["icmp_type"], c["icmp_code"] = (8 if fam == 4 else 128), 0
+                    c["event"].update(DestinationPort="", IcmpType=c["icmp_type"], IcmpCode=0)
+                out.append(c)
+    return out
+
+
+e2e_cases = []
+for it, line, tinfs, reach, protos in E2E:
+    infs = harness_infs(tinfs, protos)
+    e2e_cases.append({"it": it, "cite": f"test/e2e/functional/tests/e2e.go:{line}", "protocols": protos,
+                      "infs": infs, "interface_ingress_rules": node_state(json.loads(json.dumps(infs))),
+                      "connections": connections(reach, protos),
+                      "expect_before_policy": "reachable (XDP_PASS)", "expect_after_policy": "blocked (XDP_DROP)"})
+json.dump({
+    "source": "pbmoses/ingress-node-firewall test/e2e/functional/tests/e2e.go:176-831 (the IngressNodeFirewall table), "
+              ":1205-1352 (daemon metrics) and test/e2e/events/events.go (expected drop events), transcribed by "
+              "tests/golden/transcribe.py",
+    "assumptions": "dual-stack cluster, ENABLE_SCTP=true; synthetic pod IPs; the node interface eth0 has ifindex 2 and "
+                   "'doesntexist' is not a valid interface (loader.go:143-146 skips it); ephemeral source port 40000",
+    "ifindex": {"eth0": 2},
+    "event_regex": {  # events.go extractEventsFromString: the syslog lines a drop must produce
+        "transport": "ruleId\\s([0-9]+)\\saction\\s(?P<action>\\w+).*if\\s(?P<inf>\\w+)\n.*\\ssrc\\saddr\\s"
+                     "(?P<srcaddr>[0-9.:a-z]+)\\sdst\\saddr\\s(?P<dstaddr>[0-9.:a-z]+)\n.*(?P<proto>tcp|udp|sctp)"
+                     "\\ssrcPort\\s\\d+\\sdstPort\\s(?P<dstport>\\d+)",
+        "icmp": "ruleId\\s([0-9]+)\\saction\\s(?P<action>\\w+).*if\\s(?P<inf>\\w+)\\n.*\\s(ipv4|ipv6)\\ssrc\\saddr\\s"
+                "(?P<srcaddr>[0-9.:a-z]+)\\sdst\\saddr\\s(?P<dstaddr>[0-9.:a-z]+)\\n.*(?P<proto>icmpv4|icmpv6)\\stype"
+                "\\s(?P<type>\\d+)\\scode\\s(?P<code>\\d+)"},
+    "event_protocol": {"tcp": "TCP", "udp": "UDP", "sctp": "SCTP", "icmpv4": "ICMP", "icmpv6": "ICMPv6"},
+    "event_action": {"Drop": "Deny", "Allow": "Allow"},
+    "cases": e2e_cases,
+    "metrics": {  # e2e.go:1205-1352 "should expose daemon metrics"
+        "cite": "test/e2e/functional/tests/e2e.go:1249-1260, 1284-1299, 1331-1341",
+        "rules": [{"source_cidrs": [f"{POD_IPS[C1][0]}/32", f"{POD_IPS[C1][1]}/128"],
+                   "rules": [block_echo("ICMP", 1), block_echo("ICMPv6", 2)]}],
+        "pings": [{"src": POD_IPS[C1][0], "dst": POD_IPS[S1][0], "protocol": "ICMP", "icmp_type": 8},
+                  {"src": POD_IPS[C1][1], "dst": POD_IPS[S1][1], "protocol": "ICMPv6", "icmp_type": 128}],
+        "note": "one `ping -c 1` per family (test/e2e/icmp: ping -4/-6 -c 1), both blocked",
+        "expect": {"ingressnodefirewall_node_packet_deny_total": 2}},
+}, open("ref_e2e.json", "w"), indent=1)

@@ -287,3 +287,66 @@ def test_debug_lookup_keys_oracle():
             if k not in want:
                 want.append(k)
         assert keys == want, case["name"]
+
+
+# ---- the reference's e2e behavioural table (tests/golden/ref_e2e.json, e2e.go:176-831): TCP, UDP, SCTP, ICMP and
+# ICMPv6 block rules, a port range, multiple ports, multiple source CIDRs, multi-object merges, an invalid interface
+
+def _e2e_cases():
+    from e2e_ref import DOC
+    return DOC["cases"]
+
+
+@pytest.mark.parametrize("case", _e2e_cases(), ids=lambda c: c["cite"].split(":")[-1])
+def test_e2e_table_oracle(case):
+    """Oracle: every reachability check passes before the policy and is dropped after it, and each drop's perf
+    sample, through the consumer (events.go:77-166), yields the event the reference's e2e expects (events.go regex
+    + isEventInList)."""
+    from infw import events as E
+    from e2e_ref import DOC, case_frames, event_in_list, extract_events, if_name, packed, valid_rules
+    frames, ifx = case_frames(case["connections"])
+    m = orc.OracleMap()
+    assert [m.run(f, i)[0] for f, i in zip(frames, ifx)] == [2] * len(frames)   # initial connectivity
+    goenc.sync(m, goenc.desired(valid_rules(case["interface_ingress_rules"]), DOC["ifindex"]))
+    assert [m.run(f, i)[0] for f, i in zip(frames, ifx)] == [1] * len(frames)   # blocked
+    buf, offs, lens = packed(frames)
+    recs, samples = m.collect_event_samples(buf, offs, lens, lens, np.array(ifx, np.uint32))
+    assert recs.shape[0] == len(frames)
+    lines, log = E.drain(samples, recs.shape[0], if_name)
+    assert not log
+    got = extract_events("".join(lines))
+    for c in case["connections"]:
+        assert event_in_list(got, c["event"]), (c, lines)
+
+
+@pytest.mark.parametrize("case", _e2e_cases(), ids=lambda c: c["cite"].split(":")[-1])
+def test_e2e_table_product_controller(case):
+    """The same checks through the product's loader mirror (IngNodeFwController over the C ABI, the invalid
+    interface skipped as loader.go:143-146 does) and the compiled table image walked on the host."""
+    from e2e_ref import DOC, case_frames, controller_rules
+    from parity import stats_from_results
+    frames, ifx = case_frames(case["connections"])
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    ctl = infw.IngNodeFwController(c, if_indices=lambda name: [DOC["ifindex"][name]],
+                                   is_valid_interface=lambda name: name in DOC["ifindex"])
+    hdr, cap, pl = snapshots(frames)
+    tuples = W.pack_frames(hdr, cap, pl, np.array(ifx, np.uint32))
+    assert list(infw.verdicts_from_results(c.debug_walk(tuples), tuples[:, 6])) == [2] * len(frames)
+    ctl.ingress_node_fw_rules_loader(controller_rules(case["interface_ingress_rules"]))
+    res = c.debug_walk(tuples)
+    assert list(infw.verdicts_from_results(res, tuples[:, 6])) == [1] * len(frames)
+    st = stats_from_results(res, pl)
+    assert int(st[:, 2].sum()) == len(frames) and int(st[:, 0].sum()) == 0
+
+
+def test_e2e_metrics_oracle():
+    """e2e.go:1205-1352: one blocked ping per family -> packet_deny_total 2 (statistics.go:126-157 over rules 1..99)."""
+    from e2e_ref import DOC, conn_frame
+    doc = DOC["metrics"]
+    m = orc.OracleMap()
+    goenc.sync(m, goenc.desired({"eth0": doc["rules"]}, DOC["ifindex"]))
+    stats = np.zeros((1024, 4), np.uint64)
+    for p in doc["pings"]:
+        f = conn_frame(dict(p, icmp_code=0))
+        assert m.run(f, DOC["ifindex"]["eth0"], stats=stats)[0] == 1
+    assert int(stats[1:100, 2].sum()) == doc["expect"]["ingressnodefirewall_node_packet_deny_total"]

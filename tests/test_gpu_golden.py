@@ -137,3 +137,67 @@ def test_kernel_matches_frozen_swap():
     clf.commit()  # incremental: the live swap between two batches
     b = _gpu_record(clf, wl, n, n)
     assert a == DIG[name]["batch_a"] and b == DIG[name]["batch_b"]
+
+
+def test_e2e_table_on_device():
+    """The reference's e2e behavioural table (e2e.go:176-831, tests/golden/ref_e2e.json) on the device, no oracle:
+    for each entry the node's merged rules go through the loader mirror, the entry's reachability checks
+    (TCP/UDP/SCTP to the blocked port or range, ICMP and ICMPv6 echo requests, both families) are classified
+    straight from their frames in HBM (infw_classify_frames_ex) — all XDP_PASS before the policy, all XDP_DROP
+    after — and every drop's perf sample (infw_events_capture) through the consumer must yield the drop event the
+    reference's e2e looks for with its own regular expressions (test/e2e/events/events.go)."""
+    import ctypes as C
+    from infw import _native as N
+    from infw import events as E
+    from e2e_ref import DOC, case_frames, controller_rules, event_in_list, extract_events, if_name, packed
+    dev = torch.device("cuda", 0)
+    t32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    clf = infw.Classifier(devices=[0])
+    ctl = infw.IngNodeFwController(clf, if_indices=lambda name: [DOC["ifindex"][name]],
+                                   is_valid_interface=lambda name: name in DOC["ifindex"])
+    for case in DOC["cases"]:
+        frames, ifx = case_frames(case["connections"])
+        n = len(frames)
+        buf, offs, lens = packed(frames)
+        dbuf = torch.from_numpy(buf).to(dev)
+        doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        for phase, want in (("before", 2), ("after", 1)):
+            if phase == "before":
+                ctl.reset_all()
+            else:
+                ctl.ingress_node_fw_rules_loader(controller_rules(case["interface_ingress_rules"]))
+            ev = torch.zeros(n * C.sizeof(N.EventRec), dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            res = torch.empty(n, dtype=torch.int32, device=dev)
+            ver = torch.empty(n, dtype=torch.uint8, device=dev)
+            clf.classify_frames(dbuf, t32(lens), t32(ifx), n, results=res, verdicts=ver, offsets=doffs,
+                                events=ev, events_count=cnt)
+            smp = torch.zeros(n * N.EVENT_SAMPLE_BYTES, dtype=torch.uint8, device=dev)
+            clf.events_capture(dbuf, t32(lens), t32(ifx), n, ev, cnt, smp, offsets=doffs)
+            torch.cuda.synchronize()
+            assert list(ver.cpu().numpy()) == [want] * n, (case["it"], phase)
+            k = int(cnt.item())
+            assert k == (n if want == 1 else 0), (case["it"], phase)
+            if k:
+                lines, log = E.drain(smp.cpu().numpy(), k, if_name)
+                assert not log
+                got = extract_events("".join(lines))
+                for c in case["connections"]:
+                    assert event_in_list(got, c["event"]), (case["it"], c)
+
+
+def test_e2e_metrics_on_device():
+    """e2e.go:1205-1352: one blocked ping per family, then Statistics.update_metrics (statistics.go:112-167) over
+    the device's counters reports packet_deny_total == 2."""
+    from e2e_ref import DOC, case_frames, controller_rules
+    doc = DOC["metrics"]
+    clf = infw.Classifier(devices=[0])
+    ctl = infw.IngNodeFwController(clf, if_indices=lambda name: [DOC["ifindex"][name]])
+    ctl.ingress_node_fw_rules_loader(controller_rules({"eth0": doc["rules"]}))
+    conns = [dict(p, icmp_code=0, interface="eth0") for p in doc["pings"]]
+    frames, ifx = case_frames(conns)
+    _, ver = _device_classify(clf, frames, ifx)
+    assert list(ver) == [1, 1]
+    m = infw.Statistics(clf).update_metrics()
+    assert m["ingressnodefirewall_node_packet_deny_total"] == doc["expect"]["ingressnodefirewall_node_packet_deny_total"]
+    assert m["ingressnodefirewall_node_packet_allow_total"] == 0

@@ -6,7 +6,9 @@ size — a mix of value changes (existing and new rule lists), deletes and
 re-adds — and commits each one incrementally; then repeats the largest batch
 with INFW_F_FULL_COMMIT for comparison.  One JSON line per commit:
 host patch/compile ms, device copy ms, bytes copied to the device.
-  python tools/commit_latency.py [--host-only]
+  python tools/commit_latency.py [--host-only] [--slots N]
+--slots N: a context over N device slots of GPU 0 (devices=[0]*N, one host thread per slot at commit); the line
+also reports the slowest slot's device time.
 """
 import argparse
 import json
@@ -34,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--host-only", action="store_true")
     ap.add_argument("--sizes", default="1,10,100,1000,10000")
+    ap.add_argument("--slots", type=int, default=1)
     args = ap.parse_args()
     import infw
     from infw import workloads as W
@@ -41,7 +44,7 @@ def main():
     keys = wl.keys_bytes().reshape(-1, 24)
     tmpl = wl.templates_bytes().reshape(-1, 1200)
     flags = infw.F_HOST_ONLY if args.host_only else 0
-    devs = None if args.host_only else [0]
+    devs = None if args.host_only else [0] * args.slots
     rng = random.Random(1)
 
     def run(c, label, size):
@@ -61,6 +64,7 @@ def main():
         print(json.dumps({"commit": label, "edits": size, "mode": ["full", "incremental", "reupload"][i["commit_mode"]],
                           "wall_ms": round(wall, 2), "host_ms": round(i["compile_ms"], 2),
                           "device_ms": round(i["upload_ms"], 2), "device_bytes_copied": i["patch_bytes"],
+                          "slots": i["n_device_slots"], "slowest_slot_ms": round(i["device_ms_max"], 2),
                           "full_reason": i["full_reason"]}), flush=True)
 
     c = infw.Classifier(devices=devs, max_entries=wl.n_entries + 65536, flags=flags)

@@ -92,7 +92,8 @@ def main():
     # the traffic file bench.py reads for this workload: every figure from this one profile
     if line and "hbm_bytes_per_packet" in out:
         rates = json.load(open(os.path.join(ROOT, "profiles", "line_rates.json")))
-        tj = {"tag": tag, "workload_key": key, "kernel": line["roofline"]["kernel"], "layout": layout,
+        tj = {"tag": tag, "workload_key": key, "build_id": line.get("build_id"), "kernel": line["roofline"]["kernel"],
+              "layout": layout,
               "note": f"classify kernel, {key} bench command; see profiles/{tag}/summary.json", "line_rates": rates}
         for k in ("hbm_bytes_per_packet", "hbm_bytes_per_packet_raw", "l2_hits_per_packet", "l2_misses_per_packet",
                   "lds_bank_conflict_rate", "ea_rdreq_per_packet"):
