@@ -67,7 +67,7 @@ asan:
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build
 
-.PHONY: all clean resource-usage asm asan cachesim
+.PHONY: all clean resource-usage asm asan cachesim patch_bench
 
 # host model of the L2 behaviour of the table walk (layout experiments; tools/cachesim.cpp)
 cachesim: $(OUT)/libinfw_workload.so
@@ -75,3 +75,10 @@ cachesim: $(OUT)/libinfw_workload.so
 	g++ -std=c++17 -O2 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/cachesim.cpp $(SRC)/tables.cpp \
 	    $(SRC)/incremental.cpp $(SRC)/controlplane.cpp -L$(OUT) -linfw_workload -Wl,-rpath,$(abspath $(OUT)) \
 	    -o $(OBJ)/cachesim
+
+# host cost of incremental commits per phase (tools/patch_bench.cpp)
+patch_bench: $(OUT)/libinfw_workload.so
+	@mkdir -p $(OBJ)
+	g++ -std=c++17 -O3 -pthread -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/patch_bench.cpp \
+	    $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp $(SRC)/image.cpp -L$(OUT) -linfw_workload \
+	    -Wl,-rpath,$(abspath $(OUT)) -o $(OBJ)/patch_bench

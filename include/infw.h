@@ -221,6 +221,9 @@ int infw_table_update_batch(infw_ctx *ctx, const struct lpm_ip_key_st *keys,
                             uint64_t n, uint64_t flags, uint64_t *done);
 /* Map.Delete(key)               loader.go:640  (purgeKeys): exact prefix.    */
 int infw_table_delete(infw_ctx *ctx, const struct lpm_ip_key_st *key);
+/* Batch form (BPF_MAP_DELETE_BATCH): stops at the first error (-ENOENT for a */
+/* key not in the map); *done (may be NULL) receives the keys deleted.         */
+int infw_table_delete_batch(infw_ctx *ctx, const struct lpm_ip_key_st *keys, uint64_t n, uint64_t *done);
 /* Map.Iterate() key walk        loader.go:293,558 (getStaleKeys,            */
 /* GetBPFMapContentForTest): key==NULL or absent -> first key; -ENOENT at end. */
 /* Order is the LPM trie's post-order (children before parents, 0-bit first). */

@@ -374,8 +374,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
     __shared__ unsigned long long s_by[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
-    // diagnostic 32: no LDS word cache; the 256-thread shapes (6 blocks per CU) have no LDS room for it
-    constexpr bool kCache = !(kAblate & 32) && kBlock >= 384;
+    // diagnostic 32: no LDS word cache and no IPv6 group cache, 1024: no word cache only; the 256-thread shapes
+    // (6 blocks per CU) have no LDS room for it
+    constexpr bool kCache = !(kAblate & (32 | 1024)) && kBlock >= 384;
     constexpr uint32_t kC24 = 1u << kC24Log;
     __shared__ unsigned long long s_c24[kCache ? kC24 : 1];
     if (kCache)
@@ -704,8 +705,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         else if (G == 0 && lst) {
             // the (list, class)'s own part count when the epoch has them (infw_tables.h), else the uniform one
             uint32_t p = T.dt_plog2;
-            if (kPl) p = (s_pl[lst - 1] >> (3 * cls)) & 7u;
-            else if (T.n_dt_pl) p = (T.dt_pl[lst - 1] >> (3 * cls)) & 7u;
+            if (kPl) p = infw_dt_parts_of(s_pl[(lst - 1) & (INFW_DT_PL_LISTS - 1)], lst - 1, INFW_DT_PL_LISTS, cls, p);
+            else if (T.n_dt_pl && lst - 1 < T.n_dt_pl) p = (T.dt_pl[lst - 1] >> (3 * cls)) & 7u;
             result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2, p);
         }
         // ---- first match, one lane per rule, G packets in flight
@@ -894,6 +895,21 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
+    // LDS attribution (diagnostic, tools/lds_ablate.sh): the default lean shape without one LDS structure each —
+    // 1 the DIR-24-8 word cache, 2 the IPv6 group cache, 4 the LDS counters (no statistics: results stay valid,
+    // counters do not), 7 all three.  SQ_LDS_BANK_CONFLICT of the default minus each variant attributes the rate.
+    if (const char *e = getenv("INFW_LDS_ABLATE")) {
+        if (!in_c && group == 0 && block == 768 && bpc == 2 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS) {
+            switch (atoi(e)) {
+            case 1: launch<768, 0, 1024, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+            case 2: launch<768, 0, 0, false, 6, false, false, 11, 0, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+            case 4: launch<768, 0, 4, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+            case 7: launch<768, 0, 4 | 1024, false, 6, false, false, 11, 0, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+            default: launch<768, 0, 0, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
+            }
+            return hipGetLastError() == hipSuccess ? 0 : -5;
+        }
+    }
     const char *env_l = getenv("INFW_C24LOG");  // tuning
     const int env_log = env_l ? atoi(env_l) : 0;
     const int log = env_log ? env_log : (block == 768 ? 12 : bpc <= 3 ? 11 : 10);

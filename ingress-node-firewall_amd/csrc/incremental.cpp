@@ -45,16 +45,6 @@ struct Edit {
     uint64_t hi, lo;     // full address (masked), big-endian halves
 };
 
-// 20-byte LPM key data {ifindex LE, address bits 0..31 BE, zeros}.
-inline void short_md(uint8_t md[20], const uint8_t ifx_le[4], uint32_t a32) {
-    memset(md, 0, 20);
-    memcpy(md, ifx_le, 4);
-    md[4] = (uint8_t)(a32 >> 24);
-    md[5] = (uint8_t)(a32 >> 16);
-    md[6] = (uint8_t)(a32 >> 8);
-    md[7] = (uint8_t)a32;
-}
-
 void mark(std::vector<DirtyRange> &r, int buf, uint64_t off, uint64_t len) {
     if (len) r.push_back(DirtyRange{(uint32_t)buf, off, len});
 }
@@ -87,6 +77,12 @@ void paint(const PendingMap &m, uint32_t ifx, uint32_t a, uint32_t P, uint32_t R
         const uint64_t off = (uint64_t)(r.a32 - a) >> (32 - R);
         std::fill(ans.begin() + off, ans.begin() + off + (1ull << (R - r.L)), r.v);
     }
+}
+
+bool shorts_empty(const std::vector<Edit> &edits) {
+    for (const Edit &e : edits)
+        if (e.P <= 32) return false;
+    return true;
 }
 
 }  // namespace
@@ -297,7 +293,6 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     }
     const uint64_t n_lists_after = h.n_lists + new_vids.size();
     if (n_lists_after >= (1u << 25)) return full("more than 2^25-1 rule lists");
-    if (!h.dt_pl.empty() && n_lists_after > h.dt_pl.size()) return full("more lists than the part-count table holds");
     std::unordered_map<uint32_t, int64_t> ref_delta;  // existing lists only
     for (const Edit &e : edits) {
         if (e.was != PendingMap::kAbsent) ref_delta[inc.list_of_vid.at((uint32_t)e.was)]--;
@@ -325,9 +320,11 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (h.desc.size() < (size_t)(lid + 1) * INFW_DESC_STRIDE) h.desc.resize((size_t)(lid + 1) * INFW_DESC_STRIDE, 0);
         const size_t per_list = (size_t)INFW_NCLS << h.dt_plog2;
         if (h.dte.size() < (lid + 1) * per_list) h.dte.resize((lid + 1) * per_list, infw_dt_line{});
+        // a list past the part-count table keeps uniform parts (infw_dt_parts_of)
+        const bool pl = lid < h.dt_pl.size();
         int rc = compile_rule_list(m.pool.vals[vid].data(), h.rules, &h.desc[(size_t)lid * INFW_DESC_STRIDE],
-                                   &h.dte[lid * per_list], h.dtl, h.dt_plog2, h.dt_pl.empty() ? nullptr : &h.dt_pl[lid]);
-        if (!h.dt_pl.empty()) mark(ranges, TB_DTPL, (uint64_t)lid * 4, 4);
+                                   &h.dte[lid * per_list], h.dtl, h.dt_plog2, pl ? &h.dt_pl[lid] : nullptr);
+        if (pl) mark(ranges, TB_DTPL, (uint64_t)lid * 4, 4);
         if (rc) {
             inc.valid = false;  // the image is no longer trustworthy: the next commit recompiles
             set_error("incremental commit: decision-table leaf pool exhausted");
@@ -342,15 +339,30 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (e.now && inc.list_of_vid.at(e.now->vid) >= n_lists_before) inc.list_refs[inc.list_of_vid.at(e.now->vid)]++;
     for (const auto &d : ref_delta) inc.list_refs[d.first] = (uint64_t)((int64_t)inc.list_refs[d.first] + d.second);
     inc.dead_lists = (uint64_t)dead_after;
-    auto list1 = [&](const NodeVal *v) -> uint32_t { return v ? inc.list_of_vid.at(v->vid) + 1 : 0u; };
+    // list + 1 of a node's value: painted words repeat a few values, so a small direct-mapped memo in front of
+    // the hash map answers almost every word
+    struct Memo {
+        uint32_t vid = ~0u, l1 = 0;
+    };
+    std::array<Memo, 256> memo{};
+    auto list1 = [&](const NodeVal *v) -> uint32_t {
+        if (!v) return 0u;
+        Memo &e = memo[(v->vid * 0x9E3779B1u) >> 24];
+        if (e.vid != v->vid) e = Memo{v->vid, inc.list_of_vid.at(v->vid) + 1};
+        return e.l1;
+    };
 
     const auto tp1 = std::chrono::steady_clock::now();
+    if (!shorts_empty(edits) && inc.g8bits.size() != ((size_t)h.n_slots << 24) / 64) {
+        inc.g8bits.assign(((size_t)h.n_slots << 24) / 64, 0);
+        for (const auto &kv : h.tbl8_of) inc.g8bits[kv.first >> 6] |= 1ull << (kv.first & 63);
+    }
+    auto has_group = [&](uint64_t w) { return (inc.g8bits[w >> 6] >> (w & 63)) & 1; };
     // <= /32: shorter prefixes first, so a /25../32 group starts from its final tbl24 word
     std::vector<const Edit *> shorts;
     for (const Edit &e : edits)
         if (e.P <= 32) shorts.push_back(&e);
     std::sort(shorts.begin(), shorts.end(), [](const Edit *a, const Edit *b) { return a->P < b->P; });
-    uint8_t md[20];
     std::vector<const NodeVal *> ans, ans8;
     std::vector<PendingMap::ShortRef> tmp;
     uint64_t n_refills = 0, n_words = 0;
@@ -369,8 +381,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         uint64_t *t24 = &h.tbl24[(size_t)e->slot << 24];
         const uint64_t gkey = (uint64_t)e->slot << 24;
         const uint32_t a = e->P ? e->a32 & (~0u << (32 - e->P)) : 0u;
-        short_md(md, ifx_le, a);
-        const NodeVal *below = e->P ? m.longest(md, 32, 32 + e->P - 1) : nullptr;  // lengths < P
+        const NodeVal *below = e->P ? m.longest_short(ifx_le, a, e->P - 1) : nullptr;  // lengths < P
         const NodeVal *atP = e->now ? e->now : below;                                 // lengths <= P
         if (e->P <= 24) {
             const uint32_t i0 = a >> 8, cnt = 1u << (24 - e->P);
@@ -378,6 +389,10 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
             paint(m, ifx, a, e->P, 24, atP, ans, tmp);  // the longest entry <= /24 of every word
             for (uint32_t k = 0; k < cnt; k++) {
                 const uint32_t i = i0 + k;
+                if (!has_group(gkey | i)) {
+                    t24[i] = list1(ans[k]);
+                    continue;
+                }
                 auto g = h.tbl8_of.find(gkey | i);
                 if (g != h.tbl8_of.end()) {
                     refill_group(ifx, i, g->second, 0, 24, ans[k]);
@@ -400,6 +415,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                 std::fill(h.tbl8.begin() + ((size_t)g << 8), h.tbl8.begin() + ((size_t)g << 8) + 256, (uint32_t)t24[i]);
                 mark(ranges, TB_TBL8, ((uint64_t)g << 8) * 4, 256 * 4);
                 h.tbl8_of[gkey | i] = g;
+                inc.g8bits[(gkey | i) >> 6] |= 1ull << ((gkey | i) & 63);
                 h.n_tbl8_groups++;
             }
             refill_group(ifx, i, g, a & 0xFFu, e->P, atP);

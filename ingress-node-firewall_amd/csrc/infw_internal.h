@@ -87,6 +87,7 @@ struct PendingMap {
     PendingMap &operator=(const PendingMap &) = delete;
 
     int update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags);
+    int update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flags, const uint8_t *val = nullptr);
     // An imported committed set into an empty map (image.cpp); clear() empties the map.
     int install_committed(const ImageEntries &ent, std::string *why);
     void clear();
@@ -96,6 +97,8 @@ struct PendingMap {
     // Longest entry with minlen <= prefixLen <= maxlen covering md (20 bytes:
     // ifindex LE + address): its node, or nullptr.
     const NodeVal *longest(const uint8_t md[20], uint32_t minlen, uint32_t maxlen) const;
+    // The same for prefixLen 32..32+maxL of one ifindex (the short table's keys), through `sub`.
+    const NodeVal *longest_short(const uint8_t ifx_le[4], uint32_t a32, uint32_t maxL) const;
 };
 
 void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes);
@@ -145,6 +148,10 @@ struct IncState {
     std::unordered_map<uint32_t, uint32_t> list_of_vid;  // interned value -> rule list
     std::vector<uint64_t> list_refs;                     // entries referencing each list
     uint64_t dead_lists = 0;                             // lists no entry references any more
+    // One bit per tbl24 word (slot << 24 | /24): a tbl8 group exists for it (tbl8_of has it).  Derived from
+    // tbl8_of on the first patch after a compile or import, then kept up to date; lets a short edit skip the
+    // hash lookup for the (most common) words without a group.
+    std::vector<uint64_t> g8bits;
 };
 
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)

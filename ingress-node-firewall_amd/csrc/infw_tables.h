@@ -290,8 +290,12 @@ INFW_TD uint64_t infw_dt_slot(uint32_t list, int cls, uint32_t v, uint32_t plog2
 // Per-(list, class) part counts (n_dt_pl != 0, at most INFW_DT_PL_LISTS lists): (list, cls) keeps its region of
 // 2^dt_plog2 entry lines but is cut into only 2^p parts, the fewest whose every part fits one line (p <=
 // dt_plog2), so a packet's value lands on one of 2^p lines of the region, not 2^dt_plog2: fewer distinct lines
-// per hot (list, class).  The list's word holds p in bits [3 cls, 3 cls + 3).
+// per hot (list, class).  The list's word holds p in bits [3 cls, 3 cls + 3).  Lists appended by incremental
+// commits past the table (id >= n_dt_pl) keep the uniform 2^dt_plog2 parts.
 #define INFW_DT_PL_LISTS 4096u
+INFW_TD uint32_t infw_dt_parts_of(uint32_t word, uint32_t list, uint32_t n_dt_pl, int cls, uint32_t plog2) {
+    return list < n_dt_pl ? (word >> (3 * cls)) & 7u : plog2;
+}
 INFW_TD uint64_t infw_dt_slot_p(uint32_t list, int cls, uint32_t v, uint32_t plog2, uint32_t p) {
     return (((uint64_t)list * INFW_NCLS + (uint32_t)cls) << plog2) | (v >> (16u - p));
 }
@@ -322,7 +326,7 @@ INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
 // First-match result of (list, cls) for value v (host walk; the kernel has its own loads).
 template <class T>
 INFW_TD uint32_t infw_dt_eval(const T &t, uint32_t list, int cls, uint32_t v) {
-    const uint32_t p = t.n_dt_pl ? (t.dt_pl[list] >> (3 * cls)) & 7u : t.dt_plog2;
+    const uint32_t p = list < t.n_dt_pl ? (t.dt_pl[list] >> (3 * cls)) & 7u : t.dt_plog2;
     const uint32_t *w = t.dte[infw_dt_slot_p(list, cls, v, t.dt_plog2, p)].w;
     if (w[0] & INFW_DT_ROOT) w = t.dtl[(w[0] & INFW_DT_INDEX) + infw_keys_below(w, 1, 16, v)].w;
     return infw_dt_leaf(w, v);

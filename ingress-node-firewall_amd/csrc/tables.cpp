@@ -102,6 +102,13 @@ static NodeKey make_node(const lpm_ip_key_st *key) {
 
 // trie_update_elem (lpm_trie.c, Linux 6.18) order of checks.
 int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags) {
+    if (flags > INFW_BPF_EXIST || key->prefixLen > INFW_MAX_PREFIXLEN) return update_vid(key, 0, flags);  // errors
+    return update_vid(key, ~0u, flags, val);
+}
+
+// update() with the value already interned (vid), or interned here from val when vid == ~0u (only once the
+// checks have passed, so a refused update interns nothing).
+int PendingMap::update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flags, const uint8_t *val) {
     if (flags > INFW_BPF_EXIST) {
         set_error("update: flags > BPF_EXIST");
         return -EINVAL;
@@ -117,7 +124,7 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
         dirty.emplace(k, (int64_t)it->second.vid);  // keeps the committed state of the first edit
         memcpy(it->second.data, &key->ingress_ifindex, 4);
         memcpy(it->second.data + 4, key->ip_data, 16);
-        it->second.vid = pool.intern(val);
+        it->second.vid = vid == ~0u ? pool.intern(val) : vid;
         generation++;
         return 0;
     }
@@ -129,7 +136,7 @@ int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t fl
     NodeVal v;
     memcpy(v.data, &key->ingress_ifindex, 4);
     memcpy(v.data + 4, key->ip_data, 16);
-    v.vid = pool.intern(val);
+    v.vid = vid == ~0u ? pool.intern(val) : vid;
     dirty.emplace(k, kAbsent);
     auto ins = nodes.emplace(k, v).first;
     index_short(k, &ins->second);
@@ -203,6 +210,33 @@ const NodeVal *PendingMap::longest(const uint8_t md[20], uint32_t minlen, uint32
         if (it != nodes.end()) return &it->second;
     }
     return nullptr;
+}
+
+// longest() over the short key space of one ifindex: the entry of length L <= maxL (address bits) covering a32,
+// found through the per-block short-key lists (one list per 8 lengths, longest level first) instead of one hash
+// probe per length; L = 0 (prefixLen 32, the whole ifindex) is probed last.
+const NodeVal *PendingMap::longest_short(const uint8_t ifx_le[4], uint32_t a32, uint32_t maxL) const {
+    if (maxL > 32) maxL = 32;
+    const uint32_t ifx = rd_le32(ifx_le);
+    for (int lv = maxL ? (int)((maxL - 1) & ~7u) : -8; lv >= 0; lv -= 8) {
+        const std::vector<ShortRef> *v = sub_list((uint32_t)lv, ifx, a32);
+        if (!v) continue;
+        const NodeVal *best = nullptr;
+        uint32_t best_l = 0;
+        for (const ShortRef &r : *v)
+            if (r.L <= maxL && r.L > best_l && ((r.a32 ^ a32) >> (32 - r.L)) == 0) {
+                best = r.v;
+                best_l = r.L;
+            }
+        if (best) return best;
+    }
+    if (!len_count[32]) return nullptr;
+    NodeKey k;
+    k.plen = 32;
+    memset(k.md, 0, sizeof k.md);
+    memcpy(k.md, ifx_le, 4);
+    auto it = nodes.find(k);
+    return it == nodes.end() ? nullptr : &it->second;
 }
 
 int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {

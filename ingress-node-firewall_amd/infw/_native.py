@@ -141,6 +141,7 @@ ABI_SYMBOLS = [
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c", "infw_classify_frames",
     "infw_classify_frames_ex",
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
+    "infw_table_delete_batch",
 ]
 ABI_VERSION = 3  # include/infw.h INFW_ABI_VERSION
 
@@ -171,6 +172,7 @@ _sig = {
     "infw_table_update_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                           C.c_uint64, P(C.c_uint64)]),
     "infw_table_delete": (C.c_int, [C.c_void_p, P(LpmIpKeySt)]),
+    "infw_table_delete_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "infw_table_get_next_key": (C.c_int, [C.c_void_p, P(LpmIpKeySt), P(LpmIpKeySt)]),
     "infw_table_lookup": (C.c_int, [C.c_void_p, P(LpmIpKeySt), P(RulesValSt)]),
     "infw_table_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),

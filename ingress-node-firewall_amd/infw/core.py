@@ -95,6 +95,14 @@ class Classifier:
     def delete(self, key: LpmIpKeySt) -> None:
         check(N.lib.infw_table_delete(self._ctx, C.byref(key)), "Map.Delete")
 
+    def delete_batch_ptr(self, keys_ptr: int, n: int) -> int:
+        """infw_table_delete_batch over n packed 24-B keys at keys_ptr; returns the keys deleted (raises on the
+        first error, like BPF_MAP_DELETE_BATCH)."""
+        done = C.c_uint64(0)
+        check(N.lib.infw_table_delete_batch(self._ctx, keys_ptr, n, C.byref(done)),
+              f"Map.BatchDelete (deleted {done.value} of {n})")
+        return done.value
+
     def delete_rc(self, key: LpmIpKeySt) -> int:
         return N.lib.infw_table_delete(self._ctx, C.byref(key))
 

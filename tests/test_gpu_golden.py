@@ -151,7 +151,7 @@ def test_e2e_table_on_device():
     from infw import events as E
     from e2e_ref import DOC, case_frames, controller_rules, event_in_list, extract_events, if_name, packed
     dev = torch.device("cuda", 0)
-    t32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    t32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
     clf = infw.Classifier(devices=[0])
     ctl = infw.IngNodeFwController(clf, if_indices=lambda name: [DOC["ifindex"][name]],
                                    is_valid_interface=lambda name: name in DOC["ifindex"])

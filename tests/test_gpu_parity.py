@@ -31,6 +31,7 @@ def need_gpu():
     (W.CFG2_MIXED_1M, 1 << 19, 100000, 512),  # configs[2] shape, reduced table
     (W.CFG2_MIXED_1M, 1 << 19, 100000, 100000),  # configs[2] distinct-lists variant: one list per key
     (W.CFG4_ADVERSARIAL, 1 << 19, 20000, 64),
+    (W.CFG4_ADVERSARIAL, 1 << 19, 100000, 0),  # configs[4] at 100k prefixes (its bench default table)
 ])
 def test_parity_configs(cfg, n, npfx, ntmpl):
     r = check_cfg(cfg, n, npfx, ntmpl)
@@ -159,6 +160,66 @@ def test_full_size_properties(ntmpl):
         ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
         got = res1[start:start + (1 << 16)].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, ores), start
+
+
+def _implied_stats(res, batch, dev):
+    """Per-rule counters implied by result words (kernel.c:441-456, :376-387), with torch on the device."""
+    r = res.to(torch.int64) & 0xFFFFFFFF
+    act, key = r & 0xFF, (r >> 8) & 0xFFFF
+    plen = batch.pkt_len.to(torch.int64)
+    want = torch.zeros((1024, 4), dtype=torch.int64, device=dev)
+    for a, col in ((2, 0), (1, 2)):
+        sel = (act == a) & (key < 1024)
+        want[:, col] = torch.bincount(key[sel], minlength=1024)
+        want[:, col + 1] = torch.zeros(1024, dtype=torch.int64, device=dev).index_add_(0, key[sel], plen[sel])
+    return want
+
+
+def test_cfg4_headline_scale_live_swap():
+    """configs[4] (adversarial: /128 deepest-prefix hits, last-slot ICMPv6 type/code, aliasing keys) at the
+    headline table size — 1M generated prefixes, 1.27M entries, ~800k IPv6 /32 groups — with a live swap: batch A
+    (32M packets) on epoch 1, 2000 key edits committed incrementally, batch B on epoch 2.  Size-independent
+    properties on both batches (device counters == counters implied by the result words), and the first and last
+    64k packets of each batch bit-exact against the oracle with the identical edits applied between them."""
+    import random
+    wl = W.Workload(W.CFG4_ADVERSARIAL, n_prefixes=1000000)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 64)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    dev = torch.device("cuda", 0)
+    n = 1 << 25
+    batch = SoaBatch.empty(n, dev)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    stats = torch.zeros((1024, 4), dtype=torch.int64, device=dev)
+    keys = wl.keys_bytes().reshape(-1, 24)
+    tmpl = wl.templates_bytes().reshape(-1, 1200)
+    rng = random.Random(4)
+    for epoch, start in ((1, 0), (2, n)):
+        if epoch == 2:
+            for i in rng.sample(range(keys.shape[0]), 2000):
+                kb = keys[i].tobytes()
+                if rng.random() < 0.33:
+                    assert clf.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb)) == m.delete(kb)
+                else:
+                    vb = tmpl[rng.randrange(tmpl.shape[0])].tobytes()
+                    assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb),
+                                         infw.RulesValSt.from_buffer_copy(vb)) == m.update(kb, vb)
+            clf.commit()
+            assert clf.info()["commit_mode"] == infw.COMMIT_INCREMENTAL, clf.info()["full_reason"]
+        wl.gen_device(batch, start, 0)
+        stats.zero_()
+        clf.stats_bind(0, stats.data_ptr())
+        clf.classify(batch, results=res)
+        torch.cuda.synchronize()
+        clf.stats_bind(0, None)
+        assert torch.equal(stats, _implied_stats(res, batch, dev)), epoch
+        acts = torch.bincount((res & 0xFF).to(torch.int64), minlength=3).cpu().numpy()
+        assert acts[1] > 0 and acts[2] > 0
+        for off in (0, n - (1 << 16)):
+            hdr, cap, pl, ifx = wl.frames(start + off, 1 << 16)
+            ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+            assert np.array_equal(res[off:off + (1 << 16)].cpu().numpy().view(np.uint32), ores), (epoch, off)
 
 
 def _gpu_events(clf, batch, cap):
@@ -972,3 +1033,32 @@ def test_classify_host_batches():
         if pin:
             for a in soa.arrays():
                 clf.host_unregister(a)
+
+
+def test_lists_past_part_count_table_on_device():
+    """New rule lists committed incrementally past the per-list part-count table (> 4096 lists): the kernel's LDS
+    copy of the table covers the first 4096 lists, later ones take uniform parts — results equal the oracle."""
+    import random
+    from test_incremental_cpu import _apply, _packets_for
+    from tools_commit import new_value
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=30000, n_templates=4096)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)
+    wl.load_into(clf)
+    clf.commit()
+    m = oracle_for(wl)
+    rng = random.Random(9)
+    keys = [k for k, _ in wl.entries()]
+    dev = torch.device("cuda", 0)
+    for rnd in range(2):
+        touched = rng.sample(keys, 400)
+        for k in touched:
+            _apply([clf], m, k, new_value(rng))
+        clf.commit()
+        assert clf.info()["commit_mode"] == infw.COMMIT_INCREMENTAL, clf.info()["full_reason"]
+        hdr, cap, pl, ifx = _packets_for(touched, rng)
+        tup = W.pack_frames(hdr, cap, pl, ifx)
+        b = SoaBatch.from_tuples(tup, dev)
+        gres, _ = gpu_run(clf, b, b.n)
+        ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
+        assert np.array_equal(gres, ores), rnd
+    assert clf.info()["n_lists"] > 4096

@@ -166,3 +166,34 @@ def test_commit_reasons():
     assert c.info()["full_reason"] == "first long prefix"
     c.commit()  # nothing pending
     assert c.info()["commit_mode"] == infw.COMMIT_INCREMENTAL and c.info()["patch_bytes"] == 0
+
+
+def test_lists_past_the_part_count_table_stay_incremental():
+    """An epoch compiled with per-list part counts (<= 4096 lists, INFW_DT_PL_LISTS) takes new rule lists past the
+    table incrementally: they keep uniform value parts (infw_dt_parts_of), and the patched image classifies like
+    the oracle (round 2 recompiled the whole epoch — 2 s at configs[2] — for one new list)."""
+    import random
+    from tools_commit import new_value
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=30000, n_templates=4096)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 4096)
+    wl.load_into(c)
+    c.commit()
+    n0 = c.info()["n_lists"]
+    assert n0 > 4000
+    m = orc.OracleMap(max_entries=wl.n_entries + 4096)
+    for k, v in wl.entries():
+        m.update(k, v)
+    rng = random.Random(3)
+    keys = [k for k, _ in wl.entries()]
+    for rnd in range(3):
+        touched = rng.sample(keys, 300)
+        for k in touched:
+            _apply([c], m, k, new_value(rng))
+        c.commit()
+        i = c.info()
+        assert i["commit_mode"] == infw.COMMIT_INCREMENTAL, i["full_reason"]
+        hdr, cap, pl, ifx = _packets_for(touched[:150], rng)
+        tup = W.pack_frames(hdr, cap, pl, ifx)
+        ro, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
+        assert np.array_equal(c.debug_walk(tup), ro), rnd
+    assert c.info()["n_lists"] > max(n0, 4096)

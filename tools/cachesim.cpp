@@ -294,7 +294,7 @@ int main(int argc, char **argv) {
             }
             const uint32_t l1 = infw_lpm(t, pk, q[4], q);
             if (!l1) continue;
-            const uint32_t pl = t.n_dt_pl ? (t.dt_pl[l1 - 1] >> (3 * cls)) & 7u : t.dt_plog2;
+            const uint32_t pl = l1 - 1 < t.n_dt_pl ? (t.dt_pl[l1 - 1] >> (3 * cls)) & 7u : t.dt_plog2;
             const uint64_t key = infw_dt_slot_p(l1 - 1, cls, val, t.dt_plog2, pl);
             uint64_t &e = etag[(size_t)wg * lines + ((key * 0x9E3779B97F4A7C15ull) >> 40) % lines];
             el++;
@@ -415,7 +415,7 @@ int main(int argc, char **argv) {
                 const uint64_t ei = (uint64_t)(l1 - 1) * INFW_NCLS + cls;
                 // entry32: a list's 7 classes in 256 B (TCP, UDP, SCTP, ICMP4 | ICMP6, 58/v4, 1/v6)
                 tc[nt++] = {S_ENTRY, 3 * kSpace + (V.entry32 ? (uint64_t)(l1 - 1) * 256 + cls * 32 : ei * V.entry_stride)};
-                const uint32_t pl = t.n_dt_pl ? (t.dt_pl[l1 - 1] >> (3 * cls)) & 7u : t.dt_plog2;
+                const uint32_t pl = l1 - 1 < t.n_dt_pl ? (t.dt_pl[l1 - 1] >> (3 * cls)) & 7u : t.dt_plog2;
                 const uint64_t slot_i = infw_dt_slot_p(l1 - 1, cls, val, t.dt_plog2, pl);  // the compiled image's line
                 if (t.dt_plog2) tc[nt - 1].addr = 3 * kSpace + slot_i * 64;  // the compiled layout's entry line
                 if (t.dt_plog2 && V.pairing == 1)

@@ -1,0 +1,83 @@
+// patch_bench.cpp — host cost of incremental commits without a GPU: the pending-map edits
+// (update / delete, as infw_table_update_batch / _delete_batch apply them) and patch_tables, per phase, on a
+// BASELINE workload's full table.  Build: make patch_bench; run: build/patch_bench [cfg] [edits] [rounds]
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../ingress-node-firewall_amd/csrc/infw_internal.h"
+#include "../ingress-node-firewall_amd/csrc/workload.h"
+
+namespace infw {
+void set_error(const std::string &) {}
+}  // namespace infw
+using namespace infw;
+
+static double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+int main(int argc, char **argv) {
+    const int cfg = argc > 1 ? atoi(argv[1]) : 4;
+    const int edits = argc > 2 ? atoi(argv[2]) : 1000;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 20;
+    infw_wl *wl;
+    if (infw_wl_create(&wl, cfg, 0x1F000000ull + cfg, 0, 0)) return 1;
+    const uint64_t ne = infw_wl_n_entries(wl);
+    const lpm_ip_key_st *keys = infw_wl_keys(wl);
+    const uint32_t *vi = infw_wl_val_index(wl);
+    const rulesVal_st *tv = infw_wl_templates(wl);
+    const uint32_t nt = infw_wl_n_templates(wl);
+    PendingMap m;
+    m.max_entries = (uint32_t)ne + 65536;
+    for (uint64_t i = 0; i < ne; i++) m.update(&keys[i], reinterpret_cast<const uint8_t *>(&tv[vi[i]]), 0);
+    HostTables h;
+    IncState inc;
+    auto t = std::chrono::steady_clock::now();
+    if (compile_tables(m, h, -1, 4ull << 30, &inc)) return 1;
+    printf("cfg%d: %zu entries, compile %.0f ms\n", cfg, m.nodes.size(), ms_since(t));
+    m.dirty.clear();
+    std::mt19937_64 rng(7);
+    std::vector<double> upd, del, pat;
+    std::vector<uint32_t> vids(nt);
+    for (uint32_t j = 0; j < nt; j++) vids[j] = m.pool.intern(reinterpret_cast<const uint8_t *>(&tv[j]));
+    for (int r = 0; r < rounds; r++) {
+        std::vector<uint64_t> idx(edits);
+        for (auto &x : idx) x = rng() % ne;
+        t = std::chrono::steady_clock::now();
+        for (int k = 0; k < edits / 16; k++) m.remove(&keys[idx[k]]);
+        del.push_back(ms_since(t));
+        t = std::chrono::steady_clock::now();
+        for (int k = 0; k < edits; k++) m.update_vid(&keys[idx[k]], vids[rng() % nt], 0);
+        upd.push_back(ms_since(t));
+        std::vector<DirtyRange> ranges;
+        std::string why;
+        t = std::chrono::steady_clock::now();
+        const int rc = patch_tables(m, h, inc, ranges, &why);
+        pat.push_back(ms_since(t));
+        if (rc == 1) {  // the edit needs a full compile (counted apart)
+            printf("round %d: full compile (%s)\n", r, why.c_str());
+            pat.pop_back();
+            h = HostTables();
+            inc = IncState();
+            if (compile_tables(m, h, -1, 4ull << 30, &inc)) return 1;
+        } else if (rc) {
+            printf("round %d: patch rc %d\n", r, rc);
+            return 1;
+        }
+        m.dirty.clear();
+    }
+    auto med = [](std::vector<double> v) {
+        std::sort(v.begin(), v.end());
+        return v[v.size() / 2];
+    };
+    printf("%d edits/commit (%d deletes): update %.3f ms, delete %.3f ms, patch %.3f ms (medians of %d)\n", edits,
+           edits / 16, med(upd), med(del), med(pat), rounds);
+    infw_wl_destroy(wl);
+    return 0;
+}
