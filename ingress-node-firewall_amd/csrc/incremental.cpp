@@ -109,9 +109,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     for (const auto &kv : m.dirty) {
         Edit e;
         e.key = &kv.first;
-        auto it = m.nodes.find(kv.first);
-        e.now = it == m.nodes.end() ? nullptr : &it->second;
-        e.was = kv.second;
+        e.now = kv.second.now;
+        e.was = kv.second.was;
         if (!e.now && e.was == PendingMap::kAbsent) continue;  // added and removed again
         if (kv.first.plen < 32) return full("partial-ifindex prefix edited");
         const uint32_t ifx = rd_le32(kv.first.md);

@@ -60,9 +60,14 @@ struct PendingMap {
     ValuePool pool;
     uint64_t generation = 0;  // bumped on every successful edit
     // Keys edited since the last commit -> their committed value id (kAbsent: the
-    // key was not in the committed set).  Drives the incremental commit.
+    // key was not in the committed set) and their node now (nullptr: absent).
+    // Drives the incremental commit.
     static constexpr int64_t kAbsent = -1;
-    std::unordered_map<NodeKey, int64_t, NodeKeyHash> dirty;
+    struct DirtyEnt {
+        int64_t was;
+        const NodeVal *now;
+    };
+    std::unordered_map<NodeKey, DirtyEnt, NodeKeyHash> dirty;
     // Short keys (1..32 address bits) listed under their enclosing block: (level, ifindex, the address's top
     // `level` bits) -> the entries with level < L <= level + 8, for level 0, 8, 16, 24.  An incremental commit
     // paints the DIR-24-8 words (and tbl8 entries) an edit covers from these lists — base answer, then the

@@ -121,8 +121,8 @@ int PendingMap::update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flag
     auto it = nodes.find(k);
     if (it != nodes.end()) {
         if (flags == INFW_BPF_NOEXIST) return -EEXIST;
-        dirty.emplace(k, (int64_t)it->second.vid);  // keeps the committed state of the first edit
-        memcpy(it->second.data, &key->ingress_ifindex, 4);
+        dirty.try_emplace(k, DirtyEnt{(int64_t)it->second.vid, nullptr}).first->second.now = &it->second;  // keeps
+        memcpy(it->second.data, &key->ingress_ifindex, 4);  // the committed state of the first edit
         memcpy(it->second.data + 4, key->ip_data, 16);
         it->second.vid = vid == ~0u ? pool.intern(val) : vid;
         generation++;
@@ -137,8 +137,8 @@ int PendingMap::update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flag
     memcpy(v.data, &key->ingress_ifindex, 4);
     memcpy(v.data + 4, key->ip_data, 16);
     v.vid = vid == ~0u ? pool.intern(val) : vid;
-    dirty.emplace(k, kAbsent);
     auto ins = nodes.emplace(k, v).first;
+    dirty.try_emplace(k, DirtyEnt{kAbsent, nullptr}).first->second.now = &ins->second;
     index_short(k, &ins->second);
     order.insert(k);
     len_count[k.plen]++;
@@ -172,7 +172,7 @@ int PendingMap::remove(const lpm_ip_key_st *key) {
     NodeKey k = make_node(key);
     auto it = nodes.find(k);
     if (it == nodes.end()) return -ENOENT;
-    dirty.emplace(k, (int64_t)it->second.vid);
+    dirty.try_emplace(k, DirtyEnt{(int64_t)it->second.vid, nullptr}).first->second.now = nullptr;
     index_short(it->first, nullptr);
     nodes.erase(it);
     order.erase(k);

@@ -10,6 +10,7 @@ OUT=gpurun_out/lds_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for v in 0 1 2 4 7; do
+  mkdir -p $OUT/v$v
   for pass in kt lds; do
     if [ $pass = kt ]; then P="--kernel-trace --stats"; else P="--pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES"; fi
     INFW_LDS_ABLATE=$v timeout -k 10 300 rocprofv3 $P -d $OUT/v$v/$pass -o $pass --output-format csv -- \
