@@ -218,19 +218,35 @@ def share_tables(args, clf, wl, rank, world, use_dist, log):
     if rank == 0:
         wl.load_into(clf)
         clf.commit()
-        path[0] = f"/dev/shm/infw_bench_{os.getpid()}_{os.environ.get('MASTER_PORT', '0')}.img"
-        try:
-            size = clf.export_size()
-            with open(path[0], "w+b") as f:
-                f.truncate(size)
-                with mmap.mmap(f.fileno(), size) as mm:
-                    import ctypes as C
-                    buf = (C.c_char * size).from_buffer(mm)
-                    clf.export_into(C.addressof(buf), size)
-                    del buf
-        except OSError as e:  # no shared memory: every rank compiles
-            log(f"[bench] table image export failed ({e}); ranks compile their own tables")
-            path[0] = None
+        size = clf.export_size()
+        # shared memory when it has room (a container's /dev/shm may be small), else the temp directory; the file
+        # is allocated up front (posix_fallocate fails cleanly, where writing a mapping past a full tmpfs would
+        # SIGBUS) and nothing else is tried if neither has room: every rank then compiles
+        import tempfile
+        for d in ("/dev/shm", tempfile.gettempdir()):
+            try:
+                st = os.statvfs(d)
+                if st.f_bavail * st.f_frsize < size + (64 << 20):
+                    continue
+                p = os.path.join(d, f"infw_bench_{os.getpid()}_{os.environ.get('MASTER_PORT', '0')}.img")
+                with open(p, "w+b") as f:
+                    path[0] = p
+                    import atexit
+                    atexit.register(lambda q=p: os.path.exists(q) and os.unlink(q))  # also if a rank fails
+                    os.posix_fallocate(f.fileno(), 0, size)
+                    with mmap.mmap(f.fileno(), size) as mm:
+                        import ctypes as C
+                        buf = (C.c_char * size).from_buffer(mm)
+                        clf.export_into(C.addressof(buf), size)
+                        del buf
+                break
+            except OSError as e:
+                log(f"[bench] table image export to {d} failed ({e})")
+                if path[0]:
+                    os.unlink(path[0])
+                    path[0] = None
+        if path[0] is None:
+            log("[bench] no room for the table image: every rank compiles its own tables")
     dist.broadcast_object_list(path, src=0)
     how = "compiled"
     if rank != 0:
