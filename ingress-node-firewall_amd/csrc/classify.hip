@@ -27,6 +27,8 @@
 namespace {
 
 constexpr int kStatKeys = INFW_MAX_TARGETS;
+constexpr uint32_t kBigLen = 1u << 20;                      // frames this long skip the packed LDS counters
+constexpr unsigned long long kBytesMask = (1ull << 40) - 1;  // bytes field of a packed LDS counter
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kIfLds = 256;  // ifindex map entries mirrored in LDS
 constexpr int kC24LogDefault = 10;  // per-workgroup LDS cache of plain DIR-24-8 words: 1 << kC24Log entries
@@ -371,8 +373,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     const EventSink &ev = sb.ev;
     // IPv6 group table form: kV6 0 = one group per bucket, 1 = two-choice slots, 2 = whichever the epoch has
     const bool b2 = kV6 == 2 ? T.b2n != 0 : kV6 == 1;
-    __shared__ uint32_t s_pk[2 * kStatKeys];            // [rule][allow=0, deny=1]
-    __shared__ unsigned long long s_by[2 * kStatKeys];
+    // per-workgroup counters [rule][allow=0, deny=1], packets << 40 | bytes in one u64 (one LDS atomic per update):
+    // only frames shorter than kBigLen take this path and the workgroup flushes every kFlushTiles tiles, so
+    // neither field can carry into the other (kFlushTiles * kBlock * kBigLen < 2^40)
+    __shared__ unsigned long long s_c[2 * kStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
     // diagnostic 32: no LDS word cache and no IPv6 group cache, 1024: no word cache only; the 256-thread shapes
     // (6 blocks per CU) have no LDS room for it
@@ -396,10 +400,20 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         for (uint32_t i = threadIdx.x; i < INFW_DT_PL_LISTS; i += kBlock) s_pl[i] = T.dt_pl[i];
     if (kB6)
         for (int i = threadIdx.x; i < (int)(2u << kB6Log); i += kBlock) s_b6[i] = u32x4{0u, 0u, 0u, 0u};
-    for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) {
-        s_pk[i] = 0;
-        s_by[i] = 0;
-    }
+    for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) s_c[i] = 0;
+    // the workgroup's counters -> the device's (one u64 atomic per touched counter), zeroed for the next tiles
+    auto flush_counters = [&]() {
+        for (int s = threadIdx.x; s < 2 * kStatKeys; s += kBlock) {
+            const unsigned long long c = s_c[s];
+            if (c) {
+                unsigned long long *dst = stats + (s >> 1) * 4 + (s & 1) * 2;
+                atomicAdd(dst, c >> 40);
+                atomicAdd(dst + 1, c & kBytesMask);
+                s_c[s] = 0;
+            }
+        }
+    };
+    uint32_t tiles_since_flush = 0;
     const bool if_in_lds = T.if_mask < kIfLds;
     if (if_in_lds)
         for (uint32_t i = threadIdx.x; i <= T.if_mask; i += kBlock) {
@@ -747,8 +761,15 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         const uint32_t key = (result >> 8) & 0xFFFFu;
         if (!(kAblate & 4)) {
             // counter slot of this packet, or -1 (no stats: UNDEF, action outside {1,2}, key >= 1024)
-            const int s = (valid && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
-                              ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
+            const int s0_ = (valid && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
+                                ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
+            // a frame of kBigLen bytes or more (never a real frame) goes straight to the device counters
+            if (s0_ >= 0 && plen >= kBigLen) {
+                unsigned long long *dst = stats + (s0_ >> 1) * 4 + (s0_ & 1) * 2;
+                atomicAdd(dst, 1ull);
+                atomicAdd(dst + 1, (unsigned long long)plen);
+            }
+            const int s = plen < kBigLen ? s0_ : -1;
             // per-wavefront aggregation of the most common slot (Zipf traffic: the first eligible
             // lane's slot): its lanes are summed in registers and added once; the rest go to LDS
             const uint64_t elig = __ballot(s >= 0);
@@ -757,18 +778,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 const int s0 = __builtin_amdgcn_readlane(s, lead);
                 const bool mine = s == s0;
                 const uint64_t grp = __ballot(mine);
-                // the group's byte count: two 32-bit DPP reductions of the frame lengths' 16-bit halves (a sum of
-                // 64 halves cannot overflow 32 bits), not a 64-bit butterfly of 12 ds_bpermute (every lane active)
-                const uint32_t b_lo = mine ? plen & 0xFFFFu : 0u, b_hi = mine ? plen >> 16 : 0u;
-                const unsigned long long by = (unsigned long long)wave_sum(b_lo) + ((unsigned long long)wave_sum(b_hi) << 16);
-                if (lane == lead) {
-                    atomicAdd(&s_pk[s0], (uint32_t)__popcll(grp));
-                    atomicAdd(&s_by[s0], by);
-                }
-                if (s >= 0 && !mine) {
-                    atomicAdd(&s_pk[s], 1u);
-                    atomicAdd(&s_by[s], (unsigned long long)plen);
-                }
+                // the group's byte count: one 32-bit DPP reduction (64 frames shorter than 2^20 B sum below 2^26)
+                const uint32_t by = wave_sum(mine ? plen : 0u);
+                if (lane == lead) atomicAdd(&s_c[s0], (unsigned long long)__popcll(grp) << 40 | by);
+                if (s >= 0 && !mine) atomicAdd(&s_c[s], 1ull << 40 | plen);
             }
         }
         if (kEvents) {  // deny events (kernel.c:392-399): one atomic per wave, lanes keep their order
@@ -799,17 +812,17 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 verdicts[i] = (pk == INFW_PK_DROP_SHORT || action == INFW_XDP_DROP) ? INFW_XDP_DROP : INFW_XDP_PASS;
 
         }
+        // every workgroup runs the same number of tiles, so the barrier is uniform
+        if (!(kAblate & 4) && ++tiles_since_flush == T.stat_flush_tiles) {
+            __syncthreads();
+            flush_counters();
+            __syncthreads();
+            tiles_since_flush = 0;
+        }
     }
 
     __syncthreads();
-    for (int s = threadIdx.x; s < 2 * kStatKeys; s += kBlock) {
-        const uint32_t p = s_pk[s];
-        if (p) {
-            unsigned long long *dst = stats + (s >> 1) * 4 + (s & 1) * 2;
-            atomicAdd(dst, (unsigned long long)p);
-            atomicAdd(dst + 1, s_by[s]);
-        }
-    }
+    flush_counters();
 }
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),

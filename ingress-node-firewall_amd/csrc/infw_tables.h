@@ -179,6 +179,7 @@ struct infw_dev_tables {
     uint64_t b2n;              // != 0: btab holds the two-choice slot form with this many buckets
     const uint32_t *dt_pl;     // n_dt_pl != 0: per-list part counts, 3 bits per class (see infw_dt_slot_p)
     uint32_t n_dt_pl;
+    uint32_t stat_flush_tiles;  // classify: a workgroup flushes its LDS counters every this many tiles (<= 1024)
     const uint32_t *dxr_idx;   // short_mode INFW_SHORT_DXR: n_slots << 16 index words
     const struct infw_dt_line *dxr_lines;
 };

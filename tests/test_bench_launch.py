@@ -46,6 +46,9 @@ def test_gpus_2_spawns_two_ranks_same_digest():
     assert sum(r["packets_per_step"] for r in two["per_rank"]) == JOB
     assert one["rccl_world_size"] is None and sp1["rccl_world_size"] == 1
     assert two["config"]["stats_digest"] == one["config"]["stats_digest"] == sp1["config"]["stats_digest"]
+    four = _line(_bench("--gpus", "4", *common))  # the driver's scaling run uses 1, 2, 4, 8 ranks
+    assert four["rccl_world_size"] == 4 and four["config"]["stats_digest"] == one["config"]["stats_digest"]
+    assert [r["tables"] for r in four["per_rank"]] == ["compiled"] + ["imported"] * 3
     # the digest is the whole job's counters, walked here in one piece
     import infw
     from bench import host_counters, stats_digest

@@ -1062,3 +1062,32 @@ def test_lists_past_part_count_table_on_device():
         ores, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
         assert np.array_equal(gres, ores), rnd
     assert clf.info()["n_lists"] > 4096
+
+
+@pytest.mark.parametrize("flush_tiles", ["1", "3", None])
+def test_counter_paths(monkeypatch, flush_tiles):
+    """The packed per-workgroup LDS counters (packets << 40 | bytes) against the counters implied by the result
+    words: workgroups flushing after every tile / every 3 tiles / at the default interval, and 1 % of the frames
+    with lengths of 2^20 B or more (up to 2^32 - 1), which bypass the packed counters."""
+    if flush_tiles:
+        monkeypatch.setenv("INFW_STAT_FLUSH_TILES", flush_tiles)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    dev = torch.device("cuda", 0)
+    n = 1 << 18
+    b = SoaBatch.empty(n, dev)
+    wl.gen_device(b, 4321, 0)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    big = torch.rand(n, generator=g) < 0.01
+    lens = torch.randint(1 << 20, (1 << 32) - 1, (n,), generator=g, dtype=torch.int64)
+    pl = b.pkt_len.cpu().to(torch.int64)
+    pl[big] = lens[big]
+    b.pkt_len.copy_(pl.to(torch.int32).to(dev))  # u32 bit pattern
+    clf.stats_reset()
+    gres, _ = gpu_run(clf, b, n)
+    plen = b.pkt_len.cpu().numpy().view(np.uint32)
+    want = stats_from_results(gres, plen)
+    assert np.array_equal(clf.stats_read_all(), want)
+    assert int(want[:, 1].max()) > (1 << 32) or int(want[:, 3].max()) > (1 << 32)  # byte sums past 32 bits
