@@ -14,6 +14,7 @@ run cfg2 --steps 30
 run cfg2_compact --layout compact --no-cpu-baseline --steps 30
 run cfg1 --cfg 1 --batch 67108864 --no-cpu-baseline --steps 30
 run cfg4 --cfg 4 --no-cpu-baseline --steps 30
+run cfg4_1m --cfg 4 --prefixes 1000000 --no-cpu-baseline --steps 30
 run cfg2_uniform --uniform --no-cpu-baseline --steps 30
 run cfg2_distinct --templates 1000000 --no-cpu-baseline --steps 20
 run cfg2_frames --from-frames 128 --no-cpu-baseline --steps 20
