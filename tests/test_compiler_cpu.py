@@ -116,35 +116,37 @@ def _clustered_table(rng, n_groups=40):
     return out, anchors
 
 
+def clustered_packets(anchors, n, seed):
+    """Frames aimed at a _clustered_table: sources under its /32 anchors (IPv6 and IPv4-aliased), some on other
+    ifindexes, every protocol; (hdr, caplen, pkt_len, ifindex)."""
+    import ipaddress
+    from frames import frame, snapshots
+    r = random.Random(seed)
+    fr, ifx = [], []
+    for _ in range(n):
+        i, top = r.choice(anchors)
+        if r.random() < 0.15:
+            i = r.choice([3, 4, 5, 70000])
+        if r.random() < 0.7:
+            src = str(ipaddress.IPv6Address((top << 96) | r.getrandbits(96)))
+        elif r.random() < 0.5:
+            src = str(ipaddress.IPv4Address(top))
+        else:
+            src = str(ipaddress.IPv4Address(r.getrandbits(32)))
+        proto = r.choice(["tcp", "udp", "sctp", "icmp", "icmpv6", 1, 58, "gre"])
+        fr.append(frame(src, proto=proto, dport=r.randrange(65536), icmp_type=r.randrange(256),
+                        icmp_code=r.randrange(4), length=r.randrange(60, 1500)))
+        ifx.append(i)
+    hdr, cap, pl = snapshots(fr)
+    return hdr, cap, pl, np.array(ifx, np.uint32)
+
+
 @pytest.mark.parametrize("v6_form", ["std", "b2"])
 def test_clustered_overflow_groups(monkeypatch, v6_form):
     monkeypatch.setenv("INFW_V6_FORM", v6_form)
     rng = random.Random(7)
     entries, anchors = _clustered_table(rng)
-    from frames import frame, snapshots
-
-    def packets(n, seed):
-        r = random.Random(seed)
-        fr, ifx = [], []
-        for _ in range(n):
-            i, top = r.choice(anchors)
-            if r.random() < 0.15:
-                i = r.choice([3, 4, 5, 70000])
-            if r.random() < 0.7:
-                a = (top << 96) | r.getrandbits(96)
-                src = str(__import__("ipaddress").IPv6Address(a))
-            elif r.random() < 0.5:
-                src = str(__import__("ipaddress").IPv4Address(top))
-            else:
-                src = str(__import__("ipaddress").IPv4Address(r.getrandbits(32)))
-            proto = r.choice(["tcp", "udp", "sctp", "icmp", "icmpv6", 1, 58, "gre"])
-            fr.append(frame(src, proto=proto, dport=r.randrange(65536), icmp_type=r.randrange(256),
-                            icmp_code=r.randrange(4), length=r.randrange(60, 1500)))
-            ifx.append(i)
-        hdr, cap, pl = snapshots(fr)
-        return hdr, cap, pl, np.array(ifx, np.uint32)
-
-    c, res = walk_vs_oracle(entries, packets, n=6000)
+    c, res = walk_vs_oracle(entries, lambda n, seed: clustered_packets(anchors, n, seed), n=6000)
     info = c.info()
     assert info["n_v6_overflow"] > 0 and info["n_v6_groups"] > info["n_v6_overflow"]
     assert (res != 0).mean() > 0.3

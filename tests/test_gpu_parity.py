@@ -1091,3 +1091,46 @@ def test_counter_paths(monkeypatch, flush_tiles):
     want = stats_from_results(gres, plen)
     assert np.array_equal(clf.stats_read_all(), want)
     assert int(want[:, 1].max()) > (1 << 32) or int(want[:, 3].max()) > (1 << 32)  # byte sums past 32 bits
+
+
+@pytest.mark.parametrize("v6_form,short_table", [("std", "dir24"), ("b2", "dir24"), ("std", "compressed")])
+def test_clustered_adversarial_tables_on_device(monkeypatch, v6_form, short_table):
+    """Every LPM corner on the device (tests/test_compiler_cpu.py `_clustered_table`): IPv6 prefixes clustered
+    under few /32s (groups past 3 records: the Waldvogel overflow table, the non-lean kernel), nested lengths
+    /0../128 on three ifindexes (one above 2^16), IPv4 nesting, cross-family aliases; rule values with rule ids 0,
+    1024 and > 65535, actions outside {1, 2}, empty and reversed ranges, every protocol.  Result words, verdicts and
+    per-rule counters from the SoA kernel and the frames kernel, against the oracle."""
+    import random
+    import orc
+    from test_compiler_cpu import _clustered_table, clustered_packets
+    monkeypatch.setenv("INFW_V6_FORM", v6_form)
+    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
+    entries, anchors = _clustered_table(random.Random(7))
+    clf = infw.Classifier(devices=[0])
+    m = orc.OracleMap()
+    for k, v in entries:
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    clf.commit()
+    info = clf.info()
+    assert info["n_v6_overflow"] > 0 and info["short_mode"] == (1 if short_table == "compressed" else 0)
+    hdr, cap, pl, ifx = clustered_packets(anchors, 20000, 3)
+    ores, over, ost, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=4)
+    dev = torch.device("cuda", 0)
+    b = SoaBatch.from_tuples(W.pack_frames(hdr, cap, pl, ifx), dev)
+    clf.stats_reset()
+    gres, gver = gpu_run(clf, b, b.n)
+    assert np.array_equal(gres, ores) and np.array_equal(gver, over)
+    assert np.array_equal(clf.stats_read_all(), ost)
+    assert (ores != 0).mean() > 0.3
+    n = hdr.shape[0]
+    stride = 128
+    buf = np.zeros(n * stride, np.uint8)
+    buf.reshape(n, stride)[:, :hdr.shape[1]] = hdr
+    lin = np.minimum(cap, hdr.shape[1]).astype(np.uint32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    clf.stats_reset()
+    clf.classify_frames(torch.from_numpy(buf).to(dev), t(lin), t(ifx), n, results=res, pkt_len=t(pl), stride=stride)
+    torch.cuda.synchronize()
+    assert np.array_equal(res.cpu().numpy().view(np.uint32), ores)
+    assert np.array_equal(clf.stats_read_all(), ost)
