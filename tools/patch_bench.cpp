@@ -46,6 +46,43 @@ int main(int argc, char **argv) {
     std::vector<double> upd, del, pat;
     std::vector<uint32_t> vids(nt);
     for (uint32_t j = 0; j < nt; j++) vids[j] = m.pool.intern(reinterpret_cast<const uint8_t *>(&tv[j]));
+    auto micro = [&]() {
+    if (getenv("PB_MICRO")) {  // pieces of one update: key build + node lookup, dirty insert
+        std::vector<uint64_t> idx(edits);
+        double tf = 0, td = 0;
+        for (int r = 0; r < rounds; r++) {
+            for (auto &x : idx) x = rng() % ne;
+            t = std::chrono::steady_clock::now();
+            std::vector<NodeVal *> hit(edits);
+            for (int k = 0; k < edits; k++) {
+                const lpm_ip_key_st *key = &keys[idx[k]];
+                NodeKey nk;
+                nk.plen = key->prefixLen;
+                uint8_t d[20];
+                memcpy(d, &key->ingress_ifindex, 4);
+                memcpy(d + 4, key->ip_data, 16);
+                mask_bits(d, nk.plen, nk.md, 20);
+                hit[k] = &m.nodes.find(nk)->second;
+            }
+            tf = r ? std::min(tf, ms_since(t)) : ms_since(t);
+            t = std::chrono::steady_clock::now();
+            for (int k = 0; k < edits; k++) {
+                const lpm_ip_key_st *key = &keys[idx[k]];
+                NodeKey nk;
+                nk.plen = key->prefixLen;
+                uint8_t d[20];
+                memcpy(d, &key->ingress_ifindex, 4);
+                memcpy(d + 4, key->ip_data, 16);
+                mask_bits(d, nk.plen, nk.md, 20);
+                m.dirty.try_emplace(nk, PendingMap::DirtyEnt{0, hit[k]});
+            }
+            td = r ? std::min(td, ms_since(t)) : ms_since(t);
+            m.dirty.clear();
+        }
+        printf("micro: find %.3f ms, dirty insert %.3f ms per %d keys\n", tf, td, edits);
+    }
+    };
+    micro();
     for (int r = 0; r < rounds; r++) {
         std::vector<uint64_t> idx(edits);
         for (auto &x : idx) x = rng() % ne;
@@ -72,6 +109,7 @@ int main(int argc, char **argv) {
         }
         m.dirty.clear();
     }
+    micro();
     auto med = [](std::vector<double> v) {
         std::sort(v.begin(), v.end());
         return v[v.size() / 2];
