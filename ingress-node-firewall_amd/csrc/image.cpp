@@ -159,9 +159,10 @@ uint64_t write_image(const PendingMap &m, const HostTables &h, const IncState &i
     // entry set: the value pool in id order, then the nodes in post-order
     w.pod((uint64_t)m.pool.vals.size());
     for (const auto &v : m.pool.vals) w.put(v.data(), v.size());
-    w.pod((uint64_t)m.order.size());
-    for (const NodeKey &k : m.order) {
-        const NodeVal &v = m.nodes.at(k);
+    const std::vector<NodeKey> &order = m.ordered();
+    w.pod((uint64_t)order.size());
+    for (const NodeKey &k : order) {
+        const NodeVal &v = m.nodes.find_live(k)->val;
         w.pod(k.plen);
         w.put(k.md, sizeof k.md);
         w.put(v.data, sizeof v.data);
@@ -246,7 +247,7 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
 // The committed set as the importer's pending map: values interned in id order (distinct values, so each gets the
 // id it had), then the nodes with their ids, indexed as update() would.
 int PendingMap::install_committed(const ImageEntries &ent, std::string *why) {
-    if (!nodes.empty() || !pool.vals.empty() || !dirty.empty()) {
+    if (!nodes.empty() || !pool.vals.empty() || !dirty_ids.empty()) {
         *why = "the context already holds entries";
         return -EBUSY;
     }
@@ -261,27 +262,33 @@ int PendingMap::install_committed(const ImageEntries &ent, std::string *why) {
             return -EINVAL;
         }
     nodes.reserve(ent.nodes.size());
+    order_vec.reserve(ent.nodes.size());
     for (const auto &e : ent.nodes) {
-        auto ins = nodes.emplace(e.first, e.second);
-        if (!ins.second) {
+        const uint64_t h = NodeTable::hash(e.first);
+        if (nodes.find(e.first, h)) {
             *why = "duplicate key in the image";
             return -EINVAL;
         }
-        index_short(e.first, &ins.first->second);
-        order.insert(order.end(), e.first);  // post-order already: amortised O(1) hint
+        MapNode *n = nodes.insert(e.first, h);
+        n->val = e.second;
+        nodes.set_live(n, true);
+        index_short(e.first, &n->val);
+        order_vec.push_back(e.first);  // post-order already
         len_count[e.first.plen]++;
     }
+    if (!std::is_sorted(order_vec.begin(), order_vec.end(), PostOrderLess()))  // written in post-order; if not,
+        std::sort(order_vec.begin(), order_vec.end(), PostOrderLess());          // get_next_key still must be
     generation++;
     return 0;
 }
 
 void PendingMap::clear() {
     nodes.clear();
-    order.clear();
+    order_vec.clear();
+    order_add.clear();
     memset(len_count, 0, sizeof len_count);
-    pool.vals.clear();
-    pool.index.clear();
-    dirty.clear();
+    pool.clear();
+    dirty_ids.clear();
     sub.clear();
     generation++;
 }

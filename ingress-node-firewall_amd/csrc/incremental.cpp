@@ -94,7 +94,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         return 1;
     };
     if (!inc.valid) return full("no compiled image to patch");
-    const size_t n_edits = m.dirty.size();
+    const size_t n_edits = m.n_dirty();
     if (n_edits == 0) return 0;
     if (n_edits > std::max<size_t>(65536, m.nodes.size() / 4)) return full("too many edits");
     // a partial-ifindex prefix (prefixLen < 32) sets slot defaults under every word of the short table
@@ -106,19 +106,21 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     edits.reserve(n_edits);
     uint64_t short_words = 0;
     bool any_short = false;
-    for (const auto &kv : m.dirty) {
+    for (size_t di = 0; di < n_edits; di++) {
+        if (di + 8 < n_edits) __builtin_prefetch(&m.nodes.node(m.dirty_ids[di + 8]));
+        const MapNode &n = m.nodes.node(m.dirty_ids[di]);
         Edit e;
-        e.key = &kv.first;
-        e.now = kv.second.now;
-        e.was = kv.second.was;
+        e.key = &n.key;
+        e.now = n.live ? &n.val : nullptr;
+        e.was = n.was;
         if (!e.now && e.was == PendingMap::kAbsent) continue;  // added and removed again
-        if (kv.first.plen < 32) return full("partial-ifindex prefix edited");
-        const uint32_t ifx = rd_le32(kv.first.md);
+        if (n.key.plen < 32) return full("partial-ifindex prefix edited");
+        const uint32_t ifx = rd_le32(n.key.md);
         auto s = inc.slot_of.find(ifx);
         if (s == inc.slot_of.end()) return full("new ifindex");
         e.slot = s->second;
-        e.P = kv.first.plen - 32;
-        const uint8_t *ip = kv.first.md + 4;
+        e.P = n.key.plen - 32;
+        const uint8_t *ip = n.key.md + 4;
         e.hi = e.lo = 0;
         for (int i = 0; i < 8; i++) e.hi = e.hi << 8 | ip[i];
         for (int i = 8; i < 16; i++) e.lo = e.lo << 8 | ip[i];

@@ -5,6 +5,7 @@
 
 #include <array>
 #include <deque>
+#include <memory>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -50,29 +51,113 @@ struct ValuePool {
     std::deque<std::array<uint8_t, 1200>> vals;  // deque: growing never copies the values held
     std::unordered_multimap<uint64_t, uint32_t> index;
     uint32_t intern(const uint8_t *v);
+    // intern() with a memo of the caller's value addresses: a batch update names the same few template values
+    // call after call, and comparing one against the value its address had last time is far cheaper than
+    // hashing it (a stale address whose bytes changed fails the compare and is interned afresh).
+    uint32_t intern_at(const uint8_t *v);
+    void clear();
+
+  private:
+    struct AddrMemo {
+        const uint8_t *addr = nullptr;
+        uint32_t vid = 0;
+    };
+    std::array<AddrMemo, 1024> memo_{};
+};
+
+// One entry of the pending map, 64 B (one host cache line): key, value, and the commit bookkeeping.
+struct alignas(64) MapNode {
+    NodeKey key;
+    NodeVal val;
+    int32_t was;     // while dirty: the committed value id (PendingMap::kAbsent: not in the committed set)
+    uint32_t id;     // index in the node pool
+    uint8_t live;    // in the map (0: removed since the last commit, kept until the commit as a tombstone)
+    uint8_t dirty;   // listed in PendingMap::dirty_ids
+    uint8_t pad[6];
+};
+static_assert(sizeof(MapNode) == 64, "MapNode is one cache line");
+
+// The pending map's storage: nodes in a chunked pool (addresses never change, so the short-key lists and the
+// dirty list can point at them) and an open-addressed index of 8-B slots ((hash >> 32) << 32 | id + 1, linear
+// probing, backward-shift deletion, load <= 1/2).  A lookup is one index line and one node line, and both can
+// be prefetched ahead of a batch of keys (prefetch_slot, then prefetch_node).
+class NodeTable {
+  public:
+    static uint64_t hash(const NodeKey &k);
+    size_t size() const { return n_live_; }
+    bool empty() const { return n_live_ == 0; }
+    // The indexed node of key k (live or a tombstone), or nullptr.
+    MapNode *find(const NodeKey &k, uint64_t h) const;
+    const MapNode *find_live(const NodeKey &k) const {
+        const MapNode *n = find(k, hash(k));
+        return n && n->live ? n : nullptr;
+    }
+    // A new indexed node for key k (absent), not yet live.
+    MapNode *insert(const NodeKey &k, uint64_t h);
+    // Unindex node n and return it to the pool.
+    void erase(MapNode *n);
+    void set_live(MapNode *n, bool live) {
+        if (n->live != (uint8_t)live) n_live_ += live ? 1 : -1;
+        n->live = live;
+    }
+    void prefetch_slot(uint64_t h) const { __builtin_prefetch(&slots_[(h >> 32) & mask_]); }
+    void prefetch_node(const NodeKey &k, uint64_t h) const;
+    MapNode &node(uint32_t id) { return chunks_[id >> kChunkLog][id & (kChunk - 1)]; }
+    const MapNode &node(uint32_t id) const { return chunks_[id >> kChunkLog][id & (kChunk - 1)]; }
+    template <class F>
+    void for_each_live(F f) const {
+        for (uint32_t id = 0; id < hw_; id++) {
+            const MapNode &n = node(id);
+            if (n.live) f(n);
+        }
+    }
+    void reserve(size_t n);
+    void clear();
+
+  private:
+    static constexpr uint32_t kChunkLog = 12, kChunk = 1u << kChunkLog;
+    std::vector<uint64_t> slots_ = std::vector<uint64_t>(1024, 0);
+    uint64_t mask_ = 1023;
+    size_t n_indexed_ = 0, n_live_ = 0;
+    std::vector<std::unique_ptr<MapNode[]>> chunks_;
+    uint32_t hw_ = 0;
+    std::vector<uint32_t> free_;
+    void grow(size_t cap);
 };
 
 struct PendingMap {
     uint32_t max_entries = 0;
-    std::unordered_map<NodeKey, NodeVal, NodeKeyHash> nodes;
-    std::set<NodeKey, PostOrderLess> order;
+    NodeTable nodes;
     uint64_t len_count[INFW_MAX_PREFIXLEN + 1] = {};
     ValuePool pool;
     uint64_t generation = 0;  // bumped on every successful edit
-    // Keys edited since the last commit -> their committed value id (kAbsent: the
-    // key was not in the committed set) and their node now (nullptr: absent).
-    // Drives the incremental commit.
-    static constexpr int64_t kAbsent = -1;
-    struct DirtyEnt {
-        int64_t was;
-        const NodeVal *now;
-    };
-    std::unordered_map<NodeKey, DirtyEnt, NodeKeyHash> dirty;
+    // Keys edited since the last commit: their nodes (a removed key stays indexed as a tombstone until then), each
+    // with its committed value id (kAbsent: the key was not in the committed set).  Drives the incremental commit.
+    static constexpr int32_t kAbsent = -1;
+    std::vector<uint32_t> dirty_ids;
+    size_t n_dirty() const { return dirty_ids.size(); }
+    // After a commit: the edits are the committed state; tombstones leave the index.
+    void clear_dirty();
+    // Key order for get_next_key (trie post-order), kept lazily: a sorted vector that may still hold removed keys
+    // (and a key twice) plus the keys inserted since the last merge; next_key skips keys no longer live, and a
+    // merge drops them.  A remove costs nothing here and an insert one small-set insert (a std::set over a
+    // million keys cost ~5 us per insert or remove, in cache misses).
+    mutable std::vector<NodeKey> order_vec;
+    mutable std::set<NodeKey, PostOrderLess> order_add;
+    void order_merge() const;
+    // The live keys in post-order (merges first).
+    const std::vector<NodeKey> &ordered() const {
+        order_merge();
+        return order_vec;
+    }
+    // Prefetch the index slot / the node of a key a few iterations ahead of update or remove.
+    void prefetch_slot(const lpm_ip_key_st *key) const;
+    void prefetch_node(const lpm_ip_key_st *key) const;
     // Short keys (1..32 address bits) listed under their enclosing block: (level, ifindex, the address's top
     // `level` bits) -> the entries with level < L <= level + 8, for level 0, 8, 16, 24.  An incremental commit
     // paints the DIR-24-8 words (and tbl8 entries) an edit covers from these lists — base answer, then the
     // longer entries inside the block in ascending length — instead of probing the map per word and length.
-    // The NodeVal pointers stay valid: unordered_map never moves its elements, and a removed key leaves its list.
+    // The NodeVal pointers stay valid: pool nodes never move, and a removed key leaves its list.
     struct ShortRef {
         uint32_t a32;       // address bits 0..31, masked to L
         uint32_t L;

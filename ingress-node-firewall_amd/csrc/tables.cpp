@@ -21,18 +21,114 @@ static inline uint32_t rd_le32(const uint8_t *p) {
     return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
-static uint64_t fnv64(const uint8_t *p, size_t n, uint64_t h) {
-    for (size_t i = 0; i < n; i++) {
-        h ^= p[i];
-        h *= 0x100000001B3ull;
+// 24-B node key -> 64-bit hash: three 8-B words folded through multiply-rotate steps, then a final avalanche.
+uint64_t NodeTable::hash(const NodeKey &k) {
+    static_assert(sizeof(NodeKey) == 24, "NodeKey is 3 words");
+    uint64_t w[3];
+    memcpy(w, &k, 24);
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int i = 0; i < 3; i++) {
+        h ^= w[i] * 0xBF58476D1CE4E5B9ull;
+        h = (h << 31 | h >> 33) * 0x94D049BB133111EBull;
     }
-    h ^= h >> 31;
-    h *= 0x9E3779B97F4A7C15ull;
-    return h ^ (h >> 29);
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 32);
 }
 
-size_t NodeKeyHash::operator()(const NodeKey &k) const {
-    return (size_t)fnv64(k.md, 20, 0xCBF29CE484222325ull ^ ((uint64_t)k.plen << 40));
+size_t NodeKeyHash::operator()(const NodeKey &k) const { return (size_t)NodeTable::hash(k); }
+
+MapNode *NodeTable::find(const NodeKey &k, uint64_t h) const {
+    const uint64_t tag = h >> 32;
+    for (uint64_t i = tag & mask_;; i = (i + 1) & mask_) {
+        const uint64_t s = slots_[i];
+        if (!s) return nullptr;
+        if ((s >> 32) == tag) {
+            MapNode &n = const_cast<MapNode &>(node((uint32_t)s - 1));
+            if (n.key == k) return &n;
+        }
+    }
+}
+
+void NodeTable::prefetch_node(const NodeKey &k, uint64_t h) const {
+    (void)k;
+    const uint64_t tag = h >> 32;
+    for (uint64_t i = tag & mask_;; i = (i + 1) & mask_) {
+        const uint64_t s = slots_[i];
+        if (!s) return;
+        if ((s >> 32) == tag) {
+            __builtin_prefetch(&node((uint32_t)s - 1));
+            return;
+        }
+    }
+}
+
+void NodeTable::grow(size_t cap) {
+    std::vector<uint64_t> old(cap, 0);
+    old.swap(slots_);
+    mask_ = cap - 1;
+    for (uint64_t s : old) {
+        if (!s) continue;
+        uint64_t i = (s >> 32) & mask_;
+        while (slots_[i]) i = (i + 1) & mask_;
+        slots_[i] = s;
+    }
+}
+
+void NodeTable::reserve(size_t n) {
+    size_t cap = slots_.size();
+    while (cap < 2 * n) cap <<= 1;
+    if (cap != slots_.size()) grow(cap);
+}
+
+MapNode *NodeTable::insert(const NodeKey &k, uint64_t h) {
+    if (2 * (n_indexed_ + 1) > slots_.size()) grow(slots_.size() * 2);
+    uint32_t id;
+    if (!free_.empty()) {
+        id = free_.back();
+        free_.pop_back();
+    } else {
+        id = hw_++;
+        if ((id >> kChunkLog) >= chunks_.size()) chunks_.emplace_back(new MapNode[kChunk]());
+    }
+    MapNode &n = node(id);
+    n = MapNode{};
+    n.key = k;
+    n.id = id;
+    const uint64_t tag = h >> 32;
+    uint64_t i = tag & mask_;
+    while (slots_[i]) i = (i + 1) & mask_;
+    slots_[i] = tag << 32 | (uint64_t)(id + 1);
+    n_indexed_++;
+    return &n;
+}
+
+void NodeTable::erase(MapNode *n) {
+    const uint64_t tag = hash(n->key) >> 32;
+    uint64_t i = tag & mask_;
+    while ((uint32_t)slots_[i] != n->id + 1) i = (i + 1) & mask_;
+    // backward-shift deletion: pull later members of the probe run into the hole while their home allows it
+    for (uint64_t j = (i + 1) & mask_; slots_[j]; j = (j + 1) & mask_) {
+        const uint64_t home = (slots_[j] >> 32) & mask_;
+        const bool stays = i <= j ? (home > i && home <= j) : (home > i || home <= j);
+        if (stays) continue;
+        slots_[i] = slots_[j];
+        i = j;
+    }
+    slots_[i] = 0;
+    n_indexed_--;
+    set_live(n, false);
+    n->dirty = 0;
+    free_.push_back(n->id);
+}
+
+void NodeTable::clear() {
+    slots_.assign(1024, 0);
+    mask_ = 1023;
+    n_indexed_ = n_live_ = 0;
+    chunks_.clear();
+    hw_ = 0;
+    free_.clear();
 }
 
 static inline int bit_at(const uint8_t *d, uint32_t i) { return (d[i >> 3] >> (7 - (i & 7))) & 1; }
@@ -65,6 +161,26 @@ void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes) {
     }
 }
 
+// mask_bits over the 20 key bytes as big-endian words: the first `plen` bits kept, the rest cleared.
+static inline void mask_key20(const uint8_t *in, uint32_t plen, uint8_t *out) {
+    auto keep = [](uint32_t plen, uint32_t from) -> uint64_t {  // the top (plen - from) bits of a word
+        if (plen <= from) return 0;
+        const uint32_t b = plen - from;
+        return b >= 64 ? ~0ull : ~0ull << (64 - b);
+    };
+    uint64_t w0, w1;
+    uint32_t w2;
+    memcpy(&w0, in, 8);
+    memcpy(&w1, in + 8, 8);
+    memcpy(&w2, in + 16, 4);
+    w0 = __builtin_bswap64(__builtin_bswap64(w0) & keep(plen, 0));
+    w1 = __builtin_bswap64(__builtin_bswap64(w1) & keep(plen, 64));
+    w2 = __builtin_bswap32(__builtin_bswap32(w2) & (uint32_t)(keep(plen, 128) >> 32));
+    memcpy(out, &w0, 8);
+    memcpy(out + 8, &w1, 8);
+    memcpy(out + 16, &w2, 4);
+}
+
 // 1200-B value hash, 8 bytes per step (interning 1M distinct values hashes 1.2 GB).
 static uint64_t value_hash(const uint8_t *v) {
     uint64_t h = 0x84222325CBF29CE4ull;
@@ -90,20 +206,52 @@ uint32_t ValuePool::intern(const uint8_t *v) {
     return id;
 }
 
+uint32_t ValuePool::intern_at(const uint8_t *v) {
+    AddrMemo &e = memo_[((uintptr_t)v >> 4) * 0x9E3779B97F4A7C15ull >> 54];
+    if (e.addr == v && memcmp(vals[e.vid].data(), v, 1200) == 0) return e.vid;
+    e.addr = v;
+    e.vid = intern(v);
+    return e.vid;
+}
+
+void ValuePool::clear() {
+    vals.clear();
+    index.clear();
+    memo_.fill(AddrMemo{});
+}
+
 static NodeKey make_node(const lpm_ip_key_st *key) {
     NodeKey k;
     k.plen = key->prefixLen;
     uint8_t data[20];
     memcpy(data, &key->ingress_ifindex, 4);
     memcpy(data + 4, key->ip_data, 16);
-    mask_bits(data, k.plen, k.md, 20);
+    mask_key20(data, k.plen, k.md);
     return k;
+}
+
+void PendingMap::prefetch_slot(const lpm_ip_key_st *key) const {
+    if (key->prefixLen <= INFW_MAX_PREFIXLEN) nodes.prefetch_slot(NodeTable::hash(make_node(key)));
+}
+
+void PendingMap::prefetch_node(const lpm_ip_key_st *key) const {
+    if (key->prefixLen > INFW_MAX_PREFIXLEN) return;
+    const NodeKey k = make_node(key);
+    nodes.prefetch_node(k, NodeTable::hash(k));
 }
 
 // trie_update_elem (lpm_trie.c, Linux 6.18) order of checks.
 int PendingMap::update(const lpm_ip_key_st *key, const uint8_t *val, uint64_t flags) {
     if (flags > INFW_BPF_EXIST || key->prefixLen > INFW_MAX_PREFIXLEN) return update_vid(key, 0, flags);  // errors
     return update_vid(key, ~0u, flags, val);
+}
+
+// The first edit of a key since the last commit records its committed value.
+static inline void mark_dirty(PendingMap &m, MapNode *n, int32_t committed) {
+    if (n->dirty) return;
+    n->dirty = 1;
+    n->was = committed;
+    m.dirty_ids.push_back(n->id);
 }
 
 // update() with the value already interned (vid), or interned here from val when vid == ~0u (only once the
@@ -117,14 +265,15 @@ int PendingMap::update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flag
         set_error("update: prefixLen > 160");
         return -EINVAL;
     }
-    NodeKey k = make_node(key);
-    auto it = nodes.find(k);
-    if (it != nodes.end()) {
+    const NodeKey k = make_node(key);
+    const uint64_t h = NodeTable::hash(k);
+    MapNode *n = nodes.find(k, h);
+    if (n && n->live) {
         if (flags == INFW_BPF_NOEXIST) return -EEXIST;
-        dirty.try_emplace(k, DirtyEnt{(int64_t)it->second.vid, nullptr}).first->second.now = &it->second;  // keeps
-        memcpy(it->second.data, &key->ingress_ifindex, 4);  // the committed state of the first edit
-        memcpy(it->second.data + 4, key->ip_data, 16);
-        it->second.vid = vid == ~0u ? pool.intern(val) : vid;
+        mark_dirty(*this, n, (int32_t)n->val.vid);
+        memcpy(n->val.data, &key->ingress_ifindex, 4);  // the last writer's host bits
+        memcpy(n->val.data + 4, key->ip_data, 16);
+        n->val.vid = vid == ~0u ? pool.intern(val) : vid;
         generation++;
         return 0;
     }
@@ -133,14 +282,17 @@ int PendingMap::update_vid(const lpm_ip_key_st *key, uint32_t vid, uint64_t flag
         set_error("update: table map full");
         return -ENOSPC;
     }
-    NodeVal v;
-    memcpy(v.data, &key->ingress_ifindex, 4);
-    memcpy(v.data + 4, key->ip_data, 16);
-    v.vid = vid == ~0u ? pool.intern(val) : vid;
-    auto ins = nodes.emplace(k, v).first;
-    dirty.try_emplace(k, DirtyEnt{kAbsent, nullptr}).first->second.now = &ins->second;
-    index_short(k, &ins->second);
-    order.insert(k);
+    if (!n) {  // a tombstone (removed since the last commit) is revived instead, keeping its committed value
+        n = nodes.insert(k, h);
+        mark_dirty(*this, n, kAbsent);
+    }
+    memcpy(n->val.data, &key->ingress_ifindex, 4);
+    memcpy(n->val.data + 4, key->ip_data, 16);
+    n->val.vid = vid == ~0u ? pool.intern(val) : vid;
+    nodes.set_live(n, true);
+    index_short(k, &n->val);
+    order_add.insert(k);
+    if (order_add.size() > std::max<size_t>(4096, order_vec.size() / 8)) order_merge();
     len_count[k.plen]++;
     generation++;
     return 0;
@@ -169,16 +321,52 @@ void PendingMap::index_short(const NodeKey &k, const NodeVal *v) {
 
 int PendingMap::remove(const lpm_ip_key_st *key) {
     if (key->prefixLen > INFW_MAX_PREFIXLEN) return -EINVAL;
-    NodeKey k = make_node(key);
-    auto it = nodes.find(k);
-    if (it == nodes.end()) return -ENOENT;
-    dirty.try_emplace(k, DirtyEnt{(int64_t)it->second.vid, nullptr}).first->second.now = nullptr;
-    index_short(it->first, nullptr);
-    nodes.erase(it);
-    order.erase(k);
+    const NodeKey k = make_node(key);
+    MapNode *n = nodes.find(k, NodeTable::hash(k));
+    if (!n || !n->live) return -ENOENT;
+    mark_dirty(*this, n, (int32_t)n->val.vid);
+    index_short(n->key, nullptr);
+    nodes.set_live(n, false);  // stays indexed until the commit (clear_dirty); order entries go stale
     len_count[k.plen]--;
     generation++;
     return 0;
+}
+
+void PendingMap::clear_dirty() {
+    for (uint32_t id : dirty_ids) {
+        MapNode &n = nodes.node(id);
+        n.dirty = 0;
+        if (!n.live) nodes.erase(&n);
+    }
+    dirty_ids.clear();
+}
+
+// Merge the inserted keys into the sorted vector and drop keys no longer live (and duplicates).  Liveness is
+// checked with the index lookups pipelined (slot prefetched 16 keys ahead, node 8 ahead).
+void PendingMap::order_merge() const {
+    if (order_add.empty() && order_vec.size() <= nodes.size()) return;
+    std::vector<NodeKey> add(order_add.begin(), order_add.end());
+    order_add.clear();
+    auto live_filter = [&](std::vector<NodeKey> &v) {
+        const size_t n = v.size();
+        std::vector<uint64_t> hs(n);
+        for (size_t i = 0; i < n; i++) hs[i] = NodeTable::hash(v[i]);
+        size_t o = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (i + 16 < n) nodes.prefetch_slot(hs[i + 16]);
+            if (i + 8 < n) nodes.prefetch_node(v[i + 8], hs[i + 8]);
+            const MapNode *m = nodes.find(v[i], hs[i]);
+            if (m && m->live && (o == 0 || !(v[o - 1] == v[i]))) v[o++] = v[i];
+        }
+        v.resize(o);
+    };
+    live_filter(order_vec);
+    live_filter(add);
+    std::vector<NodeKey> out;
+    out.reserve(order_vec.size() + add.size());
+    std::merge(order_vec.begin(), order_vec.end(), add.begin(), add.end(), std::back_inserter(out), PostOrderLess());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    order_vec.swap(out);
 }
 
 int PendingMap::lookup(const lpm_ip_key_st *key, uint8_t *val) const {
@@ -191,9 +379,8 @@ int PendingMap::lookup(const lpm_ip_key_st *key, uint8_t *val) const {
         NodeKey k;
         k.plen = (uint32_t)L;
         mask_bits(data, (uint32_t)L, k.md, 20);
-        auto it = nodes.find(k);
-        if (it != nodes.end()) {
-            if (val) memcpy(val, pool.vals[it->second.vid].data(), 1200);
+        if (const MapNode *n = nodes.find_live(k)) {
+            if (val) memcpy(val, pool.vals[n->val.vid].data(), 1200);
             return 0;
         }
     }
@@ -206,8 +393,7 @@ const NodeVal *PendingMap::longest(const uint8_t md[20], uint32_t minlen, uint32
         NodeKey k;
         k.plen = (uint32_t)L;
         mask_bits(md, (uint32_t)L, k.md, 20);
-        auto it = nodes.find(k);
-        if (it != nodes.end()) return &it->second;
+        if (const MapNode *n = nodes.find_live(k)) return &n->val;
     }
     return nullptr;
 }
@@ -235,24 +421,37 @@ const NodeVal *PendingMap::longest_short(const uint8_t ifx_le[4], uint32_t a32, 
     k.plen = 32;
     memset(k.md, 0, sizeof k.md);
     memcpy(k.md, ifx_le, 4);
-    auto it = nodes.find(k);
-    return it == nodes.end() ? nullptr : &it->second;
+    const MapNode *n = nodes.find_live(k);
+    return n ? &n->val : nullptr;
 }
 
+// trie_get_next_key: the key after `key` in post-order, or the first key when `key` is absent (or NULL).
 int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
-    if (order.empty()) return -ENOENT;
-    auto it = order.begin();
+    if (nodes.empty()) return -ENOENT;
+    if (order_vec.size() > 2 * nodes.size() + 4096) order_merge();  // mostly removed keys: compact first
+    bool after = false;
+    NodeKey k{};
     if (key && key->prefixLen <= INFW_MAX_PREFIXLEN) {
-        NodeKey k = make_node(key);
-        if (nodes.count(k)) {
-            it = order.upper_bound(k);
-            if (it == order.end()) return -ENOENT;
+        k = make_node(key);
+        after = nodes.find_live(k) != nullptr;
+    }
+    const PostOrderLess less;
+    const MapNode *best = nullptr;
+    auto vi = after ? std::upper_bound(order_vec.begin(), order_vec.end(), k, less) : order_vec.begin();
+    for (; vi != order_vec.end(); ++vi)
+        if ((best = nodes.find_live(*vi))) break;
+    auto ai = after ? order_add.upper_bound(k) : order_add.begin();
+    for (; ai != order_add.end(); ++ai) {
+        if (best && !less(*ai, best->key)) break;  // the vector's candidate comes first
+        if (const MapNode *n = nodes.find_live(*ai)) {
+            best = n;
+            break;
         }
     }
-    const NodeVal &v = nodes.at(*it);
-    next->prefixLen = it->plen;
-    memcpy(&next->ingress_ifindex, v.data, 4);
-    memcpy(next->ip_data, v.data + 4, 16);
+    if (!best) return -ENOENT;
+    next->prefixLen = best->key.plen;
+    memcpy(&next->ingress_ifindex, best->val.data, 4);
+    memcpy(next->ip_data, best->val.data + 4, 16);
     return 0;
 }
 
@@ -633,11 +832,11 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     ifs.reserve(64);
     {
         std::unordered_map<uint32_t, int> seen;
-        for (const auto &kv : m.nodes) {
-            if (kv.first.plen < 32) continue;  // a partial-ifindex prefix names no interface (below)
-            uint32_t ifx = rd_le32(kv.first.md);
+        m.nodes.for_each_live([&](const MapNode &n) {
+            if (n.key.plen < 32) return;  // a partial-ifindex prefix names no interface (below)
+            uint32_t ifx = rd_le32(n.key.md);
             if (seen.emplace(ifx, 0).second) ifs.push_back(ifx);
-        }
+        });
         std::sort(ifs.begin(), ifs.end());
     }
     out.n_slots = (uint32_t)ifs.size();
@@ -691,12 +890,12 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
 
     // --- rule lists: one per distinct referenced value
     std::unordered_map<uint32_t, uint32_t> list_of_vid;
-    for (const auto &kv : m.nodes) {
-        uint32_t vid = kv.second.vid;
-        if (list_of_vid.count(vid)) continue;
+    m.nodes.for_each_live([&](const MapNode &n) {
+        const uint32_t vid = n.val.vid;
+        if (list_of_vid.count(vid)) return;
         uint32_t lid = (uint32_t)list_of_vid.size();
         list_of_vid[vid] = lid;
-    }
+    });
     out.n_lists = (uint32_t)list_of_vid.size();
     phase("slots+lists");
     reserve_slack(out.desc, (size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, inc);
@@ -800,14 +999,15 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     // from it instead of 0); an ifindex with no entries of its own takes the list of partial prefixes
     // (infw_wild_lookup), longest first.
     out.wild.clear();
-    for (const auto &kv : m.nodes)
-        if (kv.first.plen < 32) {
-            const uint8_t *d = kv.first.md;  // masked to plen bits
+    m.nodes.for_each_live([&](const MapNode &n) {
+        if (n.key.plen < 32) {
+            const uint8_t *d = n.key.md;  // masked to plen bits
             const uint32_t key = (uint32_t)d[0] << 24 | (uint32_t)d[1] << 16 | (uint32_t)d[2] << 8 | d[3];
-            out.wild.push_back(kv.first.plen);
+            out.wild.push_back(n.key.plen);
             out.wild.push_back(key);
-            out.wild.push_back(list_of_vid[kv.second.vid] + 1);
+            out.wild.push_back(list_of_vid[n.val.vid] + 1);
         }
+    });
     {
         std::vector<std::array<uint32_t, 3>> w;
         for (size_t i = 0; i < out.wild.size(); i += 3) w.push_back({out.wild[i], out.wild[i + 1], out.wild[i + 2]});
@@ -821,12 +1021,12 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     if (out.wild.empty()) out.wild.assign(3, 0u);  // never an empty device buffer
     std::vector<uint32_t> slot_default(out.n_slots, 0);
     for (uint32_t sl = 0; sl < out.n_slots; sl++) slot_default[sl] = infw_wild_match(out.wild.data(), out.n_wild, ifs[sl]);
-    for (const auto &kv : m.nodes) {
-        const NodeKey &k = kv.first;
-        if (k.plen < 32) continue;
+    m.nodes.for_each_live([&](const MapNode &n) {
+        const NodeKey &k = n.key;
+        if (k.plen < 32) return;
         uint32_t slot = slot_of[rd_le32(k.md)];
         uint32_t P = k.plen - 32;
-        uint32_t list1 = list_of_vid[kv.second.vid] + 1;
+        uint32_t list1 = list_of_vid[n.val.vid] + 1;
         const uint8_t *ip = k.md + 4;  // already masked to P bits
         if (P <= 32) {
             uint32_t a32 = (uint32_t)ip[0] << 24 | (uint32_t)ip[1] << 16 | (uint32_t)ip[2] << 8 | ip[3];
@@ -837,7 +1037,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             for (int i = 8; i < 16; i++) lo = lo << 8 | ip[i];
             longs.push_back(LongReal{slot, P, list1, hi, lo});
         }
-    }
+    });
     out.n_entries = m.nodes.size();
     phase("split");
 
@@ -1229,7 +1429,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         *inc = IncState();
         inc->slot_of = std::move(slot_of);
         inc->list_refs.assign(out.n_lists, 0);
-        for (const auto &kv : m.nodes) inc->list_refs[list_of_vid[kv.second.vid]]++;
+        m.nodes.for_each_live([&](const MapNode &n) { inc->list_refs[list_of_vid[n.val.vid]]++; });
         inc->list_of_vid = std::move(list_of_vid);
         inc->valid = true;
     }

@@ -122,6 +122,32 @@ def test_random_map_ops_match_oracle():
     assert bytes(c.next_key(K(absent))) == m.next_key(absent) == next(iter(m.keys()))
 
 
+def test_key_order_through_churn_merges_and_commits():
+    """get_next_key's lazily merged order (sorted keys + keys inserted since the last merge, removed keys skipped,
+    tombstones dropped at commit) against the oracle's post-order, past the 4096-insert merge threshold."""
+    rng = random.Random(11)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=20000)
+    m = orc.OracleMap(max_entries=20000)
+    K = infw.LpmIpKeySt.from_buffer_copy
+    vals = [bytes(rng.getrandbits(8) for _ in range(1200)) for _ in range(3)]
+    keys = list({random_key(rng) for _ in range(9000)})
+    for rnd in range(4):
+        for k in rng.sample(keys, 5000):
+            v = rng.choice(vals)
+            assert c.update_rc(K(k), infw.RulesValSt.from_buffer_copy(v), 0) == m.update(k, v, 0)
+        for k in rng.sample(keys, 2500):
+            assert c.delete_rc(K(k)) == m.delete(k)
+        if rnd % 2:
+            c.commit()
+        want = list(m.keys())
+        assert c.count() == len(want)
+        assert [bytes(k) for k, _ in c.iterate()] == want, rnd
+        for _ in range(50):  # next_key from present keys
+            i = rng.randrange(len(want))
+            nxt = c.next_key(K(want[i]))
+            assert (None if nxt is None else bytes(nxt)) == (want[i + 1] if i + 1 < len(want) else None)
+
+
 def test_commit_epoch_counts():
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
     e0 = c.info()["epoch"]

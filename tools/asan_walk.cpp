@@ -117,7 +117,7 @@ static int run_churn(int n_keys, int seed) {
     HostTables h;
     IncState inc;
     if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
-    m.dirty.clear();
+    m.clear_dirty();
     int patched = 0, full = 0;
     const int rounds = getenv("ASAN_CHURN_ROUNDS") ? atoi(getenv("ASAN_CHURN_ROUNDS")) : 8;
     for (int round = 0; round < rounds; round++) {
@@ -156,7 +156,7 @@ static int run_churn(int n_keys, int seed) {
                 }
             }
         }
-        m.dirty.clear();
+        m.clear_dirty();
         HostTables f;
         if (compile_tables(m, f, INFW_SHORT_DIR24, 4ull << 30)) return -1;
         const infw_dev_tables tp = h.view(), tf = f.view();

@@ -41,56 +41,48 @@ int main(int argc, char **argv) {
     auto t = std::chrono::steady_clock::now();
     if (compile_tables(m, h, -1, 4ull << 30, &inc)) return 1;
     printf("cfg%d: %zu entries, compile %.0f ms\n", cfg, m.nodes.size(), ms_since(t));
-    m.dirty.clear();
+    m.clear_dirty();
     std::mt19937_64 rng(7);
     std::vector<double> upd, del, pat;
     std::vector<uint32_t> vids(nt);
     for (uint32_t j = 0; j < nt; j++) vids[j] = m.pool.intern(reinterpret_cast<const uint8_t *>(&tv[j]));
-    auto micro = [&]() {
-    if (getenv("PB_MICRO")) {  // pieces of one update: key build + node lookup, dirty insert
+    auto micro = [&]() {  // node lookups alone: one after the other, and pipelined as the batch calls run them
+        if (!getenv("PB_MICRO")) return;
         std::vector<uint64_t> idx(edits);
-        double tf = 0, td = 0;
+        double tf = 0, tp = 0;
+        uint64_t found = 0;
         for (int r = 0; r < rounds; r++) {
             for (auto &x : idx) x = rng() % ne;
-            t = std::chrono::steady_clock::now();
-            std::vector<NodeVal *> hit(edits);
-            for (int k = 0; k < edits; k++) {
-                const lpm_ip_key_st *key = &keys[idx[k]];
-                NodeKey nk;
-                nk.plen = key->prefixLen;
-                uint8_t d[20];
-                memcpy(d, &key->ingress_ifindex, 4);
-                memcpy(d + 4, key->ip_data, 16);
-                mask_bits(d, nk.plen, nk.md, 20);
-                hit[k] = &m.nodes.find(nk)->second;
+            for (int pass = 0; pass < 2; pass++) {
+                t = std::chrono::steady_clock::now();
+                for (int k = 0; k < edits; k++) {
+                    if (pass && k + 16 < edits) m.prefetch_slot(&keys[idx[k + 16]]);
+                    if (pass && k + 8 < edits) m.prefetch_node(&keys[idx[k + 8]]);
+                    found += m.lookup(&keys[idx[k]], nullptr) == 0;
+                }
+                double &d = pass ? tp : tf;
+                d = r ? std::min(d, ms_since(t)) : ms_since(t);
             }
-            tf = r ? std::min(tf, ms_since(t)) : ms_since(t);
-            t = std::chrono::steady_clock::now();
-            for (int k = 0; k < edits; k++) {
-                const lpm_ip_key_st *key = &keys[idx[k]];
-                NodeKey nk;
-                nk.plen = key->prefixLen;
-                uint8_t d[20];
-                memcpy(d, &key->ingress_ifindex, 4);
-                memcpy(d + 4, key->ip_data, 16);
-                mask_bits(d, nk.plen, nk.md, 20);
-                m.dirty.try_emplace(nk, PendingMap::DirtyEnt{0, hit[k]});
-            }
-            td = r ? std::min(td, ms_since(t)) : ms_since(t);
-            m.dirty.clear();
         }
-        printf("micro: find %.3f ms, dirty insert %.3f ms per %d keys\n", tf, td, edits);
-    }
+        printf("micro: %d lookups %.3f ms, pipelined %.3f ms (%llu found)\n", edits, tf, tp, (unsigned long long)found);
     };
     micro();
     for (int r = 0; r < rounds; r++) {
         std::vector<uint64_t> idx(edits);
         for (auto &x : idx) x = rng() % ne;
         t = std::chrono::steady_clock::now();
-        for (int k = 0; k < edits / 16; k++) m.remove(&keys[idx[k]]);
+        for (int k = 0; k < edits / 16; k++) {  // as infw_table_delete_batch / _update_batch run them
+            if (k + 16 < edits / 16) m.prefetch_slot(&keys[idx[k + 16]]);
+            if (k + 8 < edits / 16) m.prefetch_node(&keys[idx[k + 8]]);
+            m.remove(&keys[idx[k]]);
+        }
         del.push_back(ms_since(t));
         t = std::chrono::steady_clock::now();
-        for (int k = 0; k < edits; k++) m.update_vid(&keys[idx[k]], vids[rng() % nt], 0);
+        for (int k = 0; k < edits; k++) {
+            if (k + 16 < edits) m.prefetch_slot(&keys[idx[k + 16]]);
+            if (k + 8 < edits) m.prefetch_node(&keys[idx[k + 8]]);
+            m.update_vid(&keys[idx[k]], vids[rng() % nt], 0);
+        }
         upd.push_back(ms_since(t));
         std::vector<DirtyRange> ranges;
         std::string why;
@@ -107,7 +99,7 @@ int main(int argc, char **argv) {
             printf("round %d: patch rc %d\n", r, rc);
             return 1;
         }
-        m.dirty.clear();
+        m.clear_dirty();
     }
     micro();
     auto med = [](std::vector<double> v) {
