@@ -26,6 +26,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <thread>
+
 #include "infw_internal.h"
 
 namespace infw {
@@ -78,6 +80,29 @@ void paint(const PendingMap &m, uint32_t ifx, uint32_t a, uint32_t P, uint32_t R
         std::fill(ans.begin() + off, ans.begin() + off + (1ull << (R - r.L)), r.v);
     }
 }
+
+// The records of one IPv6 group while it is edited: at most INFW_BUCKET_INLINE, plus one before the check that
+// refuses a fourth — inline, no allocation per group.
+struct SmallRecs {
+    infw_v6_rec r[INFW_BUCKET_INLINE + 1];
+    uint32_t n = 0;
+    infw_v6_rec *begin() { return r; }
+    infw_v6_rec *end() { return r + n; }
+    const infw_v6_rec *begin() const { return r; }
+    const infw_v6_rec *end() const { return r + n; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    infw_v6_rec &operator[](size_t i) { return r[i]; }
+    void push_back(const infw_v6_rec &x) { r[n++] = x; }
+    void assign(const infw_v6_rec *a, const infw_v6_rec *b) {
+        n = (uint32_t)(b - a);
+        std::copy(a, b, r);
+    }
+    void erase(infw_v6_rec *from, infw_v6_rec *to) {
+        std::copy(to, end(), from);
+        n -= (uint32_t)(to - from);
+    }
+};
 
 bool shorts_empty(const std::vector<Edit> &edits) {
     for (const Edit &e : edits)
@@ -134,16 +159,25 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     if (any_short && h.short_mode != INFW_SHORT_DIR24) return full("short table is not DIR-24-8");
     if (short_words > (1ull << 22)) return full("edits cover too much of the short table");
 
+    const auto tpb = std::chrono::steady_clock::now();
     // IPv6 long prefixes: the final record set of every touched (slot, /32) group
     struct Group {
         uint64_t bucket;  // btab index (found or insert position)
         bool found;
-        std::vector<infw_v6_rec> recs;
+        SmallRecs recs;
         uint32_t b2k = 0, b2n = 0;  // two-choice slot form: first slot and record count of the group
     };
     std::unordered_map<uint64_t, Group> groups;
+    groups.reserve(edits.size());
     const uint64_t bmask = h.btab.size() - 1;
     uint64_t new_buckets = 0;
+    // every long edit's first bucket line, requested before the groups are read (a few hundred lines: they
+    // arrive while the loop below starts, instead of one miss after another)
+    for (const Edit &e : edits) {
+        if (e.P <= 32 || h.levels.empty()) continue;
+        const uint64_t hh = infw_bucket_hash(e.slot, e.a32);
+        __builtin_prefetch(h.b2n ? &h.btab[INFW_B2_INDEX(hh >> 32, h.b2n)] : &h.btab[hh & bmask]);
+    }
     for (const Edit &e : edits) {
         if (e.P <= 32) continue;
         if (h.levels.empty()) return full("first long prefix");
@@ -284,22 +318,35 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (std::adjacent_find(pos.begin(), pos.end()) != pos.end()) return full("IPv6 bucket probe collision");
     }
 
+    const auto tpc = std::chrono::steady_clock::now();
     // lists: values not compiled yet, and the reference counts after the edits
+    if (inc.lid_of_vid.empty() && !inc.list_of_vid.empty()) {
+        uint32_t top = 0;
+        for (const auto &kv : inc.list_of_vid) top = std::max(top, kv.first + 1);
+        inc.lid_of_vid.assign(std::max<size_t>(top, m.pool.vals.size()), ~0u);
+        for (const auto &kv : inc.list_of_vid) inc.lid_of_vid[kv.first] = kv.second;
+    }
+    auto lid_of = [&](uint32_t vid) -> uint32_t { return vid < inc.lid_of_vid.size() ? inc.lid_of_vid[vid] : ~0u; };
     std::vector<uint32_t> new_vids;
     {
         std::unordered_map<uint32_t, int> seen;
         for (const Edit &e : edits)
-            if (e.now && !inc.list_of_vid.count(e.now->vid) && seen.emplace(e.now->vid, 0).second)
+            if (e.now && lid_of(e.now->vid) == ~0u && seen.emplace(e.now->vid, 0).second)
                 new_vids.push_back(e.now->vid);
     }
     const uint64_t n_lists_after = h.n_lists + new_vids.size();
     if (n_lists_after >= (1u << 25)) return full("more than 2^25-1 rule lists");
     std::unordered_map<uint32_t, int64_t> ref_delta;  // existing lists only
+    ref_delta.reserve(2 * edits.size());
     for (const Edit &e : edits) {
-        if (e.was != PendingMap::kAbsent) ref_delta[inc.list_of_vid.at((uint32_t)e.was)]--;
+        if (e.was != PendingMap::kAbsent) {
+            const uint32_t l = lid_of((uint32_t)e.was);
+            if (l == ~0u) return full("committed value without a rule list");  // cannot happen: recompile
+            ref_delta[l]--;
+        }
         if (e.now) {
-            auto l = inc.list_of_vid.find(e.now->vid);
-            if (l != inc.list_of_vid.end()) ref_delta[l->second]++;
+            const uint32_t l = lid_of(e.now->vid);
+            if (l != ~0u) ref_delta[l]++;
         }
     }
     int64_t dead_after = (int64_t)inc.dead_lists;
@@ -315,6 +362,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     for (uint32_t vid : new_vids) {
         const uint32_t lid = h.n_lists++;
         inc.list_of_vid[vid] = lid;
+        if (vid >= inc.lid_of_vid.size()) inc.lid_of_vid.resize(std::max<size_t>(vid + 1, m.pool.vals.size()), ~0u);
+        inc.lid_of_vid[vid] = lid;
         inc.list_refs.push_back(0);
         const size_t r0 = h.rules.size(), l0 = h.dtl.size();
         // the image always holds >= 1 list slot: list 0 may be the placeholder of an empty epoch
@@ -337,7 +386,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         mark(ranges, TB_DTL, l0 * sizeof(infw_dt_line), (h.dtl.size() - l0) * sizeof(infw_dt_line));
     }
     for (const Edit &e : edits)  // references of the lists just created (ref_delta holds the older ones)
-        if (e.now && inc.list_of_vid.at(e.now->vid) >= n_lists_before) inc.list_refs[inc.list_of_vid.at(e.now->vid)]++;
+        if (e.now && lid_of(e.now->vid) >= n_lists_before) inc.list_refs[lid_of(e.now->vid)]++;
     for (const auto &d : ref_delta) inc.list_refs[d.first] = (uint64_t)((int64_t)inc.list_refs[d.first] + d.second);
     inc.dead_lists = (uint64_t)dead_after;
     // list + 1 of a node's value: painted words repeat a few values, so a small direct-mapped memo in front of
@@ -345,15 +394,91 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     struct Memo {
         uint32_t vid = ~0u, l1 = 0;
     };
-    std::array<Memo, 256> memo{};
-    auto list1 = [&](const NodeVal *v) -> uint32_t {
+    std::array<Memo, 256> memo{}, memo6{};  // one per phase (the IPv6 phase may run on a second thread)
+    auto list1_in = [&](std::array<Memo, 256> &mm, const NodeVal *v) -> uint32_t {
         if (!v) return 0u;
-        Memo &e = memo[(v->vid * 0x9E3779B1u) >> 24];
-        if (e.vid != v->vid) e = Memo{v->vid, inc.list_of_vid.at(v->vid) + 1};
+        Memo &e = mm[(v->vid * 0x9E3779B1u) >> 24];
+        if (e.vid != v->vid) e = Memo{v->vid, lid_of(v->vid) + 1};
         return e.l1;
+    };
+    auto list1 = [&](const NodeVal *v) { return list1_in(memo, v); };
+
+    // IPv6 buckets.  Touches only btab, n_buckets, the groups and their plan (the short-table phase below only
+    // the DIR-24-8 words, tbl8 groups and g8bits; both read the map), so with enough of both kinds of edits it
+    // runs on a second thread beside the short-table phase.
+    std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
+    for (const auto &kv : inc.slot_of) ifx_of_slot[kv.second] = kv.first;
+    std::vector<DirtyRange> ranges6;
+    auto v6_phase = [&]() {
+        auto list1 = [&](const NodeVal *v) { return list1_in(memo6, v); };
+        auto &ranges = ranges6;
+        // the entry of every record of the touched groups ({ifindex, address bits 0..127} at its length), looked up
+        // with the index slot prefetched 16 records ahead and the node 8 ahead
+        struct RecKey {
+            NodeKey k;
+            uint64_t h;
+            infw_v6_rec *r;
+        };
+        std::vector<RecKey> rks;
+        rks.reserve(groups.size() * 2);
+        for (auto &kv : groups) {
+            Group &g = kv.second;
+            if (!g.found && g.recs.empty()) continue;
+            const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
+            for (infw_v6_rec &r : g.recs) {
+                uint8_t kmd[20];
+                const uint32_t L = (r.meta >> 25) + 32;
+                memcpy(kmd, &ifx_of_slot[slot], 4);
+                const uint64_t hi = (uint64_t)top << 32 | r.mid;
+                for (int i = 0; i < 8; i++) kmd[4 + i] = (uint8_t)(hi >> (56 - 8 * i));
+                for (int i = 0; i < 8; i++) kmd[12 + i] = (uint8_t)(r.lo >> (56 - 8 * i));
+                RecKey rk;
+                rk.k.plen = L + 32;
+                mask_bits(kmd, L + 32, rk.k.md, 20);
+                rk.h = NodeTable::hash(rk.k);
+                rk.r = &r;
+                rks.push_back(rk);
+            }
+        }
+        for (size_t i = 0; i < rks.size(); i++) {
+            if (i + 16 < rks.size()) m.nodes.prefetch_slot(rks[i + 16].h);
+            if (i + 8 < rks.size()) m.nodes.prefetch_node(rks[i + 8].k, rks[i + 8].h);
+            const MapNode *n = m.nodes.find(rks[i].k, rks[i].h);
+            rks[i].r->meta = (rks[i].k.plen - 64) << 25 | list1(n && n->live ? &n->val : nullptr);
+        }
+        for (auto &kv : groups) {
+            Group &g = kv.second;
+            if (!g.found && g.recs.empty()) continue;
+            const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
+            std::sort(g.recs.begin(), g.recs.end(), [](const infw_v6_rec &a, const infw_v6_rec &c) { return a.meta > c.meta; });
+            if (h.b2n) {  // the planned slots, longest record first
+                auto &b = plan.count(g.bucket) ? plan[g.bucket] : *reinterpret_cast<std::array<infw_v6_slot, 2> *>(
+                                                                       h.btab.data() + g.bucket);
+                for (size_t k = 0; k < g.recs.size(); k++) b[g.b2k + k].rec = g.recs[k];
+                mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
+                continue;
+            }
+            infw_v6_bucket &b = h.btab[g.bucket];
+            if (!g.found) {
+                b.tag = slot + 1;
+                b.top = top;
+                h.n_buckets++;
+            }
+            b.n = (uint32_t)g.recs.size();
+            memset(b.rec, 0, sizeof(b.rec));
+            for (size_t k = 0; k < g.recs.size(); k++) b.rec[k] = g.recs[k];
+            mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
+        }
+        for (const auto &kv : plan) {  // two-choice slot form: the planned buckets
+            memcpy(h.btab.data() + kv.first, kv.second.data(), sizeof(infw_v6_bucket));
+            mark(ranges, TB_BTAB, kv.first * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
+        }
     };
 
     const auto tp1 = std::chrono::steady_clock::now();
+    const bool split = !groups.empty() && !shorts_empty(edits) && edits.size() >= 256;
+    std::thread t6;
+    if (split) t6 = std::thread(v6_phase);
     if (!shorts_empty(edits) && inc.g8bits.size() != ((size_t)h.n_slots << 24) / 64) {
         inc.g8bits.assign(((size_t)h.n_slots << 24) / 64, 0);
         for (const auto &kv : h.tbl8_of) inc.g8bits[kv.first >> 6] |= 1ull << (kv.first & 63);
@@ -426,48 +551,12 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     }
 
     const auto tp2 = std::chrono::steady_clock::now();
-    // IPv6 buckets
-    std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
-    for (const auto &kv : inc.slot_of) ifx_of_slot[kv.second] = kv.first;
-    for (auto &kv : groups) {
-        Group &g = kv.second;
-        if (!g.found && g.recs.empty()) continue;
-        const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
-        for (infw_v6_rec &r : g.recs) {
-            uint8_t kmd[20];
-            // the record's entry: {ifindex, address bits 0..127} at its length
-            const uint32_t L = (r.meta >> 25) + 32;
-            memset(kmd, 0, 20);
-            memcpy(kmd, &ifx_of_slot[slot], 4);
-            const uint64_t hi = (uint64_t)top << 32 | r.mid;
-            for (int i = 0; i < 8; i++) kmd[4 + i] = (uint8_t)(hi >> (56 - 8 * i));
-            for (int i = 0; i < 8; i++) kmd[12 + i] = (uint8_t)(r.lo >> (56 - 8 * i));
-            const NodeVal *v = m.longest(kmd, L + 32, L + 32);
-            r.meta = (L - 32) << 25 | list1(v);
-        }
-        std::sort(g.recs.begin(), g.recs.end(), [](const infw_v6_rec &a, const infw_v6_rec &c) { return a.meta > c.meta; });
-        if (h.b2n) {  // the planned slots, longest record first
-            auto &b = plan.count(g.bucket) ? plan[g.bucket] : *reinterpret_cast<std::array<infw_v6_slot, 2> *>(
-                                                                   h.btab.data() + g.bucket);
-            for (size_t k = 0; k < g.recs.size(); k++) b[g.b2k + k].rec = g.recs[k];
-            mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
-            continue;
-        }
-        infw_v6_bucket &b = h.btab[g.bucket];
-        if (!g.found) {
-            b.tag = slot + 1;
-            b.top = top;
-            h.n_buckets++;
-        }
-        b.n = (uint32_t)g.recs.size();
-        memset(b.rec, 0, sizeof(b.rec));
-        for (size_t k = 0; k < g.recs.size(); k++) b.rec[k] = g.recs[k];
-        mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
+    if (split) {
+        t6.join();
+    } else {
+        v6_phase();
     }
-    for (const auto &kv : plan) {  // two-choice slot form: the planned buckets
-        memcpy(h.btab.data() + kv.first, kv.second.data(), sizeof(infw_v6_bucket));
-        mark(ranges, TB_BTAB, kv.first * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
-    }
+    ranges.insert(ranges.end(), ranges6.begin(), ranges6.end());
     h.n_buckets = (uint64_t)((int64_t)h.n_buckets + b2_delta);
     h.n_entries = m.nodes.size();
     if (getenv("INFW_PATCH_TRACE")) {
@@ -475,6 +564,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         for (const Edit *e : shorts) minP = std::min(minP, e->P);
         const auto tp3 = std::chrono::steady_clock::now();
         auto ms = [](auto d) { return std::chrono::duration<double, std::milli>(d).count(); };
+        fprintf(stderr, "[patch] checks: scan %.3f, groups %.3f, lists %.3f ms\n", ms(tpb - tpa), ms(tpc - tpb), ms(tp0 - tpc));
         fprintf(stderr, "[patch] %zu edits: checks %.2f ms, lists %.2f ms (%zu new), shorts %.2f ms (%zu, shortest /%u; %llu tbl24 words, %llu tbl8 refills), "
                 "IPv6 groups %.2f ms (%zu)\n", edits.size(), ms(tp0 - tpa), ms(tp1 - tp0), new_vids.size(), ms(tp2 - tp1),
                 shorts.size(), minP, (unsigned long long)n_words, (unsigned long long)n_refills, ms(tp3 - tp2), groups.size());

@@ -242,6 +242,9 @@ struct IncState {
     // tbl8_of on the first patch after a compile or import, then kept up to date; lets a short edit skip the
     // hash lookup for the (most common) words without a group.
     std::vector<uint64_t> g8bits;
+    // list_of_vid as a dense vector (vid -> list, ~0u: none), derived on the first patch after a compile or
+    // import and kept up to date by the patch: a commit looks every edited key's old and new list up.
+    std::vector<uint32_t> lid_of_vid;
 };
 
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)

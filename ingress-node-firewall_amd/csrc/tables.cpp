@@ -152,7 +152,10 @@ bool PostOrderLess::operator()(const NodeKey &a, const NodeKey &b) const {
     return a.plen > b.plen;  // descendant (longer) before ancestor; equal -> false
 }
 
+static inline void mask_key20(const uint8_t *in, uint32_t plen, uint8_t *out);
+
 void mask_bits(const uint8_t *in, uint32_t plen, uint8_t *out, int nbytes) {
+    if (nbytes == 20) return mask_key20(in, plen, out);
     for (int i = 0; i < nbytes; i++) {
         uint32_t b0 = 8u * (uint32_t)i;
         if (plen >= b0 + 8) out[i] = in[i];

@@ -122,7 +122,8 @@ def test_incremental_churn_matches_oracle_and_full(monkeypatch, v6_form):
 
 
 def test_incremental_on_workload_table():
-    """configs[2] shape (100k prefixes): small edit batches stay incremental and bit-exact."""
+    """configs[2] shape (100k prefixes): small edit batches stay incremental and bit-exact (300 mixed IPv4 / IPv6
+    edits per commit: the IPv6 bucket phase runs on its own thread beside the short-table phase)."""
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=100000, n_templates=512)
     ents = list(wl.entries())
     inc = infw.Classifier(flags=infw.F_HOST_ONLY)

@@ -49,7 +49,20 @@ def main():
     torch.cuda.synchronize()
     rng = np.random.default_rng(7)
 
+    def edit_sets(edits):
+        """Per batch: `edits` existing keys rewritten with other rule lists (one batch update), 1/16 of them deleted
+        first and re-added by that update — drawn before the timed loop (the syncer's diff is an input here)."""
+        out = []
+        for _ in range(args.batches):
+            idx = rng.integers(keys.shape[0], size=edits)  # repeats are fine
+            dels = np.ascontiguousarray(keys[np.unique(idx[: edits // 16])])  # every key is present
+            sel = np.ascontiguousarray(keys[idx])
+            vi = rng.integers(tmpl.shape[0], size=edits).astype(np.uint32)
+            out.append((dels, sel, vi))
+        return out
+
     def run(edits):
+        sets = edit_sets(edits) if edits else None
         clf.stats_reset()
         commit_ms = []
         torch.cuda.synchronize()
@@ -57,13 +70,10 @@ def main():
         edit_ms = []
         for k in range(args.batches):
             clf.classify(batches[k & 1], results=res)
-            if edits:  # rewrite `edits` existing keys with other rule lists (one batch update), delete + re-add 1/16
+            if edits:
                 e0 = time.perf_counter()
-                idx = rng.integers(keys.shape[0], size=edits)  # O(edits); repeats are fine
-                dels = np.ascontiguousarray(keys[np.unique(idx[: edits // 16])])  # every key is present: the batch
-                clf.delete_batch_ptr(dels.ctypes.data, dels.shape[0])             # update below re-adds them
-                sel = np.ascontiguousarray(keys[idx])
-                vi = rng.integers(tmpl.shape[0], size=edits).astype(np.uint32)
+                dels, sel, vi = sets[k]
+                clf.delete_batch_ptr(dels.ctypes.data, dels.shape[0])
                 clf.update_batch_ptr(sel.ctypes.data, tmpl.ctypes.data, vi.ctypes.data, edits)
                 c0 = time.perf_counter()
                 edit_ms.append((c0 - e0) * 1e3)
