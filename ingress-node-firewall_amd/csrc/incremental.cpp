@@ -110,7 +110,25 @@ bool shorts_empty(const std::vector<Edit> &edits) {
     return true;
 }
 
+void derive_lid_of_vid(IncState &inc) {
+    uint32_t top = 0;
+    for (const auto &kv : inc.list_of_vid) top = std::max(top, kv.first + 1);
+    inc.lid_of_vid.assign(top, ~0u);
+    for (const auto &kv : inc.list_of_vid) inc.lid_of_vid[kv.first] = kv.second;
+}
+
+void derive_g8bits(const HostTables &h, IncState &inc) {
+    inc.g8bits.assign(((size_t)h.n_slots << 24) / 64, 0);
+    for (const auto &kv : h.tbl8_of) inc.g8bits[kv.first >> 6] |= 1ull << (kv.first & 63);
+}
+
 }  // namespace
+
+void patch_prepare(const HostTables &h, IncState &inc) {
+    if (!inc.valid) return;
+    derive_lid_of_vid(inc);
+    if (h.short_mode == INFW_SHORT_DIR24) derive_g8bits(h, inc);
+}
 
 int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
                  std::string *why) {
@@ -320,12 +338,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
 
     const auto tpc = std::chrono::steady_clock::now();
     // lists: values not compiled yet, and the reference counts after the edits
-    if (inc.lid_of_vid.empty() && !inc.list_of_vid.empty()) {
-        uint32_t top = 0;
-        for (const auto &kv : inc.list_of_vid) top = std::max(top, kv.first + 1);
-        inc.lid_of_vid.assign(std::max<size_t>(top, m.pool.vals.size()), ~0u);
-        for (const auto &kv : inc.list_of_vid) inc.lid_of_vid[kv.first] = kv.second;
-    }
+    if (inc.lid_of_vid.empty() && !inc.list_of_vid.empty()) derive_lid_of_vid(inc);
     auto lid_of = [&](uint32_t vid) -> uint32_t { return vid < inc.lid_of_vid.size() ? inc.lid_of_vid[vid] : ~0u; };
     std::vector<uint32_t> new_vids;
     {
@@ -479,10 +492,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     const bool split = !groups.empty() && !shorts_empty(edits) && edits.size() >= 256;
     std::thread t6;
     if (split) t6 = std::thread(v6_phase);
-    if (!shorts_empty(edits) && inc.g8bits.size() != ((size_t)h.n_slots << 24) / 64) {
-        inc.g8bits.assign(((size_t)h.n_slots << 24) / 64, 0);
-        for (const auto &kv : h.tbl8_of) inc.g8bits[kv.first >> 6] |= 1ull << (kv.first & 63);
-    }
+    if (!shorts_empty(edits) && inc.g8bits.size() != ((size_t)h.n_slots << 24) / 64) derive_g8bits(h, inc);
     auto has_group = [&](uint64_t w) { return (inc.g8bits[w >> 6] >> (w & 63)) & 1; };
     // <= /32: shorter prefixes first, so a /25../32 group starts from its final tbl24 word
     std::vector<const Edit *> shorts;

@@ -274,6 +274,9 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
 // nothing was modified), < 0 on error.
 int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
                  std::string *why);
+// The patch's derived indexes (g8bits, lid_of_vid) of a freshly compiled or imported image, built up front so the
+// first incremental commit after it does not pay for them (~5 ms at configs[2]).
+void patch_prepare(const HostTables &h, IncState &inc);
 
 // Class-filtered GPU rule records of one 1200-B value (appended to rules) and
 // the per-class first-match decision-table entry lines, INFW_NCLS << plog2 of
