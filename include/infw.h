@@ -470,7 +470,11 @@ struct infw_table_info {
                                /* commit (wall, host thread of that slot)      */
     uint32_t n_device_slots;   /* slots the last commit published to            */
     uint32_t imported;         /* 1: the epoch came from infw_table_import      */
-    uint64_t reserved[14];     /* zero; future fields come out of this         */
+    uint32_t d16;              /* 1: /16 words in front of DIR-24-8 (sparse     */
+                               /* short tables; chosen per full compile)       */
+    uint32_t d16_permille;     /* of the /16s holding a prefix longer than /16, */
+                               /* those a /16 word answers alone               */
+    uint64_t reserved[13];     /* zero; future fields come out of this         */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
 #define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */

@@ -53,17 +53,22 @@ __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t
 
 // kLean: the epoch has no compressed short table (DIR-24-8 or none), no overflowed IPv6 group and no
 // partial-ifindex prefix (infw_dev_tables.lean), so those paths are compiled out.
-template <bool kCache, int kLog, bool kLean = false>
+// kD16: the epoch has /16 words in front of DIR-24-8 (infw_tables.h); a /16 they answer needs no tbl24 word.
+template <bool kCache, int kLog, bool kLean = false, bool kD16 = false>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
                                                         unsigned long long *s_c24) {
     if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u)
-        return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? infw_dir24_lookup(T, slot, a32)
+        return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? (kD16 ? infw_d16_lookup(T, slot, a32) : infw_dir24_lookup(T, slot, a32))
                         : T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, slot, a32) : 0u)
                      : infw_short_lookup(T, slot, a32);
     const uint32_t key = slot << 24 | a32 >> 8;
     const uint32_t idx = (key * 0x9E3779B1u) >> (32 - kLog);
     const unsigned long long e = s_c24[idx];
     if ((e >> 63) && (uint32_t)(e >> 31) == key) return (uint32_t)e & 0x7FFFFFFFu;
+    if (kD16) {
+        const uint64_t d = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
+        if (d & INFW_D16_INLINE) return infw_d16_value(d, a32 & 0xFFFFu);
+    }
     const uint64_t w = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
     if (w & INFW_D24_GROUP) {
         if (w & INFW_D24_INLINE) return infw_d24_inline(w, a32 & 0xFFu);
@@ -364,7 +369,8 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false>
+          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false,
+          bool kD16 = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -650,6 +656,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                                 lng = B[3] & 0x1FFFFFFu;
                         }
                     }
+                    // /16 words (kD16): an IPv4 lane the LDS cache did not answer reads its /16 word in this round
+                    // instead of the tbl24 word, and the tbl24 word only when the /16 word does not answer
+                    const bool needd = kD16 && need24;
+                    uint64_t wd = 0;
+                    if (needd) {
+                        need24 = false;
+                        wd = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
+                    }
                     if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
                     if (needx) wx = T.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
                     if (need6) {
@@ -657,6 +671,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
                         bh = b[0];
                         br0 = b[1];
+                    }
+                    if (needd) {
+                        if (wd & INFW_D16_INLINE) {
+                            sh = infw_d16_value(wd, a32 & 0xFFFFu);
+                        } else {
+                            need24 = true;
+                            w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
+                        }
                     }
                     if (need6) {
                         lng = b2 ? v6_finish_b2<kLean>(T, (uint32_t)slot, a32, sw, bhash, bi, bh, br0)
@@ -697,7 +719,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         sh = kLean ? (T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, (uint32_t)slot, a32) : 0u)
                                    : infw_short_lookup(T, (uint32_t)slot, a32);
                     }
-                    if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log, kLean>(T, (uint32_t)slot, a32, s_c24);
+                    if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log, kLean, kD16>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 } else if (slot >= 0) {  // diagnostic 512: the sequential form (bucket round, then tbl24 round)
                     const uint32_t a32 = infw_bswap32(sa.x);
@@ -827,14 +849,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false, int kV6 = 2, bool kPl = false>
+          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -854,6 +876,11 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
     // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form; with
     // per-list part counts their LDS copy takes half the word cache (INFW_DT_ADAPT=0 at compile: none)
+    // sparse short tables with /16 words (d16_on), with and without per-list part counts
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on && T->n_dt_pl == INFW_DT_PL_LISTS)
+        launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on)
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
         launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)

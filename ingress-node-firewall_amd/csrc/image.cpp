@@ -121,6 +121,9 @@ void tables_io(IO &io, M &h) {  // HostTables fields, in one order for both dire
     io.vec(h.dt_pl);
     io.vec(h.dxr_idx);
     io.vec(h.dxr_lines);
+    io.vec(h.d16);
+    io.pod(h.d16_on);
+    io.pod(h.d16_permille);
     io.pod(h.n_lists);
     io.pod(h.n_entries);
     io.pod(h.n_long_entries);

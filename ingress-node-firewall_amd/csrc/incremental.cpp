@@ -560,6 +560,25 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         }
     }
 
+    // /16 words in front of DIR-24-8 (d16_on): re-derived for every /16 an edit covers, from the words just painted
+    if (h.d16_on && !shorts.empty()) {
+        std::vector<uint64_t> blocks;  // slot << 16 | /16
+        for (const Edit *e : shorts) {
+            const uint32_t a = e->P ? e->a32 & (~0u << (32 - e->P)) : 0u;
+            const uint32_t cnt = e->P >= 16 ? 1u : 1u << (16 - e->P);
+            for (uint32_t k = 0; k < cnt; k++) blocks.push_back((uint64_t)e->slot << 16 | ((a >> 16) + k));
+        }
+        std::sort(blocks.begin(), blocks.end());
+        blocks.erase(std::unique(blocks.begin(), blocks.end()), blocks.end());
+        for (size_t i = 0; i < blocks.size();) {
+            size_t j = i;
+            for (; j < blocks.size() && blocks[j] == blocks[i] + (j - i); j++)
+                h.d16[blocks[j]] = d16_word(h, (uint32_t)(blocks[j] >> 16), (uint32_t)blocks[j] & 0xFFFFu);
+            mark(ranges, TB_D16, blocks[i] * 8, (uint64_t)(j - i) * 8);
+            i = j;
+        }
+    }
+
     const auto tp2 = std::chrono::steady_clock::now();
     if (split) {
         t6.join();

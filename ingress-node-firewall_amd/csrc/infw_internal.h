@@ -223,6 +223,9 @@ struct HostTables {
     std::vector<uint32_t> dt_pl;         // per-list part counts (INFW_DT_PL_LISTS words) or empty (infw_tables.h)
     std::vector<uint32_t> dxr_idx;       // short_mode INFW_SHORT_DXR: index words (infw_tables.h)
     std::vector<infw_dt_line> dxr_lines; //   and range lines
+    std::vector<uint64_t> d16;           // d16_on: n_slots << 16 /16 words in front of DIR-24-8 (infw_tables.h)
+    uint32_t d16_on = 0;
+    uint32_t d16_permille = 0;           // of the /16s holding a prefix longer than /16, those with an inline word
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -247,6 +250,12 @@ struct IncState {
     std::vector<uint32_t> lid_of_vid;
 };
 
+// The /16 word of (slot, address bits 0..15) from the DIR-24-8 image: inline when its runs fit, else 0.
+// *runs: 1 for a /16 of one answer throughout (either way).
+uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs = nullptr);
+// Decide whether the epoch gets /16 words (INFW_D16=0/1 forces) and build them.
+void build_d16(HostTables &h);
+
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
 int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,
                    uint64_t dir24_budget = 4ull << 30, IncState *inc = nullptr);
@@ -254,7 +263,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1
 // The device-resident buffers of one image, in upload order.
 enum TableBuf {
     TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
-    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_DXRI, TB_DXRL, TB_COUNT
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_DXRI, TB_DXRL, TB_D16, TB_COUNT
 };
 // Host bytes of buffer b (at least one element, like the upload).
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);

@@ -182,6 +182,8 @@ struct infw_dev_tables {
     uint32_t stat_flush_tiles;  // classify: a workgroup flushes its LDS counters every this many tiles (<= 1024)
     const uint32_t *dxr_idx;   // short_mode INFW_SHORT_DXR: n_slots << 16 index words
     const struct infw_dt_line *dxr_lines;
+    const uint64_t *d16;       // d16_on: n_slots << 16 words in front of DIR-24-8 (INFW_D16_*)
+    uint32_t d16_on;
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -453,6 +455,27 @@ INFW_TD uint32_t infw_dir24_lookup(const T &t, uint32_t slot, uint32_t a32) {
     return t.tbl8[((uint64_t)(uint32_t)e << 8) | (a32 & 0xFFu)];
 }
 
+// /16 words in front of DIR-24-8 (d16_on; chosen per full compile when most /16s that hold any prefix longer
+// than /16 are of the shape below, e.g. sparse tables of /16../32 prefixes).  One 8-B word per (slot, address
+// bits 0..15), 512 KiB per slot — small enough to stay in L2 — where DIR-24-8 spreads a /16../23 prefix over
+// up to 256 words on 16 lines of its 128 MiB per slot.  Bit 63 set: the /16 holds at most three runs of the
+// shape A | B | A, values <= 0x7FFF: A bits 0..14, B 15..29, b bits 30..45, e 46..61, and address bits 16..31 x
+// -> x in [b, e] ? B : A.  Bit 63 clear: the /16 is read from its DIR-24-8 word (which stays complete, so a
+// reader that ignores the /16 words is still exact).
+#define INFW_D16_INLINE (1ull << 63)
+INFW_TD uint32_t infw_d16_value(uint64_t w, uint32_t lo16) {
+    const uint32_t b = (uint32_t)(w >> 30) & 0xFFFFu, e = (uint32_t)(w >> 46) & 0xFFFFu;
+    return (uint32_t)(w >> (lo16 >= b && lo16 <= e ? 15 : 0)) & 0x7FFFu;
+}
+INFW_TD uint64_t infw_d16_encode(uint32_t A, uint32_t B, uint32_t b, uint32_t e) {
+    return INFW_D16_INLINE | (uint64_t)e << 46 | (uint64_t)b << 30 | (uint64_t)B << 15 | A;
+}
+template <class T>
+INFW_TD uint32_t infw_d16_lookup(const T &t, uint32_t slot, uint32_t a32) {
+    const uint64_t w = t.d16[((uint64_t)slot << 16) | (a32 >> 16)];
+    return (w & INFW_D16_INLINE) ? infw_d16_value(w, a32 & 0xFFFFu) : infw_dir24_lookup(t, slot, a32);
+}
+
 template <class T>
 INFW_TD uint32_t infw_dir_lookup(const T &t, uint32_t slot, uint32_t a32) {
     uint32_t e = t.l16[((uint64_t)slot << 16) | (a32 >> 16)];
@@ -549,7 +572,7 @@ INFW_TD uint32_t infw_dxr_lookup(const T &t, uint32_t slot, uint32_t a32) {
 
 template <class T>
 INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
-    if (t.short_mode == INFW_SHORT_DIR24) return infw_dir24_lookup(t, slot, a32);
+    if (t.short_mode == INFW_SHORT_DIR24) return t.d16_on ? infw_d16_lookup(t, slot, a32) : infw_dir24_lookup(t, slot, a32);
     if (t.short_mode == INFW_SHORT_DXR) return infw_dxr_lookup(t, slot, a32);
     return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }

@@ -1193,6 +1193,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.dxr_idx.clear();
         out.dxr_lines.clear();
     }
+    build_d16(out);
     if (out.dxr_idx.empty()) out.dxr_idx.push_back(INFW_DXR_DIRECT);
     if (out.dxr_lines.empty()) out.dxr_lines.push_back(infw_dt_line{});
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
@@ -1440,6 +1441,82 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     return 0;
 }
 
+uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs) {
+    const uint64_t *w = &h.tbl24[((size_t)slot << 24) | (size_t)hi << 8];
+    uint32_t v[3] = {0, 0, 0}, st[3] = {0, 0, 0}, nr = 0;
+    bool fits = true;
+    auto push = [&](uint32_t start, uint32_t val) {
+        if (nr && v[nr - 1] == val) return;
+        if (nr == 3) {
+            fits = false;
+            return;
+        }
+        st[nr] = start;
+        v[nr++] = val;
+    };
+    for (uint32_t i = 0; i < 256 && fits; i++) {
+        const uint64_t e = w[i];
+        if (!(e & INFW_D24_GROUP)) {
+            push(i << 8, (uint32_t)e);
+        } else if (e & INFW_D24_INLINE) {  // the word's runs start at 0 and at its (at most two) boundaries
+            const uint32_t b1 = (e & INFW_D24_ABA) ? (uint32_t)(e >> 44) & 0xFFu : (uint32_t)(e >> 45) & 0xFFu;
+            const uint32_t b2 = (e & INFW_D24_ABA) ? (uint32_t)(e >> 52) & 0x1FFu : (uint32_t)(e >> 53) & 0xFFu;
+            push(i << 8, infw_d24_inline(e, 0));
+            if (b1 < 256) push(i << 8 | b1, infw_d24_inline(e, b1));
+            if (b2 < 256) push(i << 8 | b2, infw_d24_inline(e, b2));
+        } else {
+            const uint32_t *g = &h.tbl8[(size_t)(uint32_t)e << 8];
+            for (uint32_t x = 0; x < 256 && fits; x++) push(i << 8 | x, g[x]);
+        }
+    }
+    if (runs) *runs = fits ? nr : 4u;
+    if (!fits || v[0] > 0x7FFFu || v[1] > 0x7FFFu || (nr == 3 && v[2] != v[0])) return 0;
+    if (nr == 1) return infw_d16_encode(v[0], v[0], 0, 0xFFFFu);
+    return infw_d16_encode(v[0], v[1], st[1], nr == 3 ? st[2] - 1 : 0xFFFFu);
+}
+
+void build_d16(HostTables &h) {
+    h.d16_on = 0;
+    h.d16_permille = 0;
+    h.d16.clear();
+    const char *env = getenv("INFW_D16");
+    const int req = env ? atoi(env) : -1;
+    if (h.short_mode == INFW_SHORT_DIR24 && h.tbl24.size() == ((size_t)h.n_slots << 24) && h.n_slots && req != 0) {
+        std::vector<uint64_t> d((size_t)h.n_slots << 16);
+        std::vector<uint64_t> cnt(2 * (size_t)h.n_slots, 0);  // per slot: /16s with structure, of them inline
+        auto one = [&](uint32_t s) {
+            for (uint32_t b = 0; b < 65536; b++) {
+                uint32_t nr = 0;
+                const uint64_t w = d16_word(h, s, b, &nr);
+                d[((size_t)s << 16) | b] = w;
+                cnt[2 * s] += nr > 1;
+                cnt[2 * s + 1] += nr > 1 && w;
+            }
+        };
+        const uint32_t nt = std::min<uint32_t>(h.n_slots, 16);
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < nt; t++)
+            th.emplace_back([&, t] {
+                for (uint32_t s = t; s < h.n_slots; s += nt) one(s);
+            });
+        for (uint32_t s = 0; s < h.n_slots; s += nt) one(s);
+        for (auto &x : th) x.join();
+        uint64_t structured = 0, inl = 0;
+        for (uint32_t s = 0; s < h.n_slots; s++) {
+            structured += cnt[2 * s];
+            inl += cnt[2 * s + 1];
+        }
+        h.d16_permille = structured ? (uint32_t)(inl * 1000 / structured) : 1000u;
+        // worth a word in front of DIR-24-8 when most /16s with structure inside are answered by it: a lookup that
+        // falls through reads both (one more dependent L2 round trip)
+        if (req == 1 || h.d16_permille >= 500) {
+            h.d16 = std::move(d);
+            h.d16_on = 1;
+        }
+    }
+    if (h.d16.empty()) h.d16.push_back(0);
+}
+
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
 #define INFW_HB(v) \
     *p = h.v.data(); \
@@ -1464,6 +1541,7 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
     case TB_DTPL: INFW_HB(dt_pl);
     case TB_DXRI: INFW_HB(dxr_idx);
     case TB_DXRL: INFW_HB(dxr_lines);
+    case TB_D16: INFW_HB(d16);
     default:
         *p = nullptr;
         *bytes = 0;
@@ -1505,6 +1583,8 @@ infw_dev_tables HostTables::view() const {
     t.n_dt_pl = (uint32_t)dt_pl.size();
     t.dxr_idx = dxr_idx.data();
     t.dxr_lines = dxr_lines.data();
+    t.d16 = d16.data();
+    t.d16_on = d16_on;
     return t;
 }
 

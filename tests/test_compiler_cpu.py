@@ -59,6 +59,57 @@ def test_workloads(monkeypatch, cfg, npfx, ntmpl, v6_form):
         assert (c.info()["v6_slot_buckets"] > 0) == (v6_form == "b2")
 
 
+@pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG1_V4_10K, 0, 0), (W.CFG2_MIXED_1M, 100000, 512),
+                                            (W.CFG4_ADVERSARIAL, 20000, 64)])
+@pytest.mark.parametrize("d16", ["0", "1"])
+def test_workloads_d16_words(monkeypatch, cfg, npfx, ntmpl, d16):
+    """/16 words in front of DIR-24-8 forced off / on (INFW_D16): the host walk (which reads them like the
+    kernel) equals the oracle either way."""
+    monkeypatch.setenv("INFW_D16", d16)
+    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
+    c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n), n=30000)
+    info = c.info()
+    assert info["d16"] == int(d16)
+    assert d16 == "0" or info["d16_permille"] > 0
+
+
+def test_d16_chosen_for_sparse_short_tables(monkeypatch):
+    """The automatic choice: configs[1] (10k /16../32 prefixes, one per /16 mostly) gets /16 words; a /16 packed
+    with many BGP-like prefixes of several lists does not."""
+    monkeypatch.delenv("INFW_D16", raising=False)
+    wl = W.Workload(W.CFG1_V4_10K)
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    for k, v in wl.entries():
+        c.update(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v))
+    c.commit()
+    assert c.info()["d16"] == 1 and c.info()["d16_permille"] > 800
+    rng = random.Random(3)
+    ents = []
+    for b in range(64):  # 64 /16s, each holding 40 /24s and /28s of 8 lists: 4+ runs per /16
+        for j in range(40):
+            L = rng.choice([24, 28])
+            a = (10 << 24) | (b << 16) | (rng.randrange(256) << 8) | (rng.randrange(16) << 4)
+            k = struct.pack("<II", L + 32, 5) + a.to_bytes(4, "big") + b"\0" * 12
+            ents.append((k, _val(random.Random(j % 8), 1)))
+    c2, _ = walk_vs_oracle(ents, lambda n, s: _v4_frames_in(ents, n, s))
+    assert c2.info()["d16"] == 0 and c2.info()["d16_permille"] < 500
+
+
+def _v4_frames_in(ents, n, seed):
+    from frames import frame, snapshots
+    rng = random.Random(seed)
+    fr, ifx = [], []
+    for _ in range(n):
+        k, _ = rng.choice(ents)
+        plen, i = struct.unpack("<II", k[:8])
+        a = int.from_bytes(k[8:12], "big") | rng.getrandbits(32 - (plen - 32))
+        fr.append(frame("%d.%d.%d.%d" % tuple(a.to_bytes(4, "big")), proto=rng.choice(["tcp", "udp"]),
+                        dport=rng.randrange(65536), length=100))
+        ifx.append(i)
+    hdr, cap, pl = snapshots(fr)
+    return hdr, cap, pl, np.array(ifx, np.uint32)
+
+
 def test_distinct_lists_parallel_compile(monkeypatch):
     """configs[2]'s distinct-lists variant (one 1200-B value per key, loader.go:158-161) at 12k keys: the
     rule lists compile on host threads (>= 4096 lists) into thread-local pools that are rebased; the walk

@@ -403,6 +403,19 @@ def test_parity_range_short_table(monkeypatch):
     assert_parity(r, "cfg4-dxr")
 
 
+@pytest.mark.parametrize("d16", ["0", "1"])
+def test_parity_d16_words(monkeypatch, d16):
+    """/16 words in front of DIR-24-8 (infw_tables.h; INFW_D16 forces them on or off, the compiler chooses them
+    for sparse short tables such as configs[1] and [4]): bit-identical either way, on configs[1], [2] (100k
+    prefixes, and the full 1M table, where the compiler would not choose them) and [4]."""
+    monkeypatch.setenv("INFW_D16", d16)
+    for cfg, n, npfx, ntmpl, start in [(W.CFG1_V4_10K, 1 << 18, 0, 0, 0), (W.CFG2_MIXED_1M, 1 << 18, 100000, 512, 0),
+                                       (W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64, 0),
+                                       (W.CFG2_MIXED_1M, 1 << 17, 0, 0, (1 << 26) + 777)]:
+        r = check_cfg(cfg, n, npfx, ntmpl, start=start)
+        assert_parity(r, f"cfg{cfg}-{npfx}-d16={d16}")
+
+
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""

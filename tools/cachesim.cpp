@@ -53,8 +53,8 @@ struct L2 {
     }
 };
 
-enum Struct { S_BUCKET, S_TBL24, S_TBL8, S_ENTRY, S_LEAF, S_N };
-const char *kName[S_N] = {"bucket", "tbl24", "tbl8", "entry", "leaf"};
+enum Struct { S_BUCKET, S_TBL24, S_TBL8, S_ENTRY, S_LEAF, S_D16, S_N };
+const char *kName[S_N] = {"bucket", "tbl24", "tbl8", "entry", "leaf", "d16"};
 
 struct Touch {
     int s;
@@ -77,7 +77,35 @@ struct Variant {
     int adapt = 0;    // 1: per-(list, class) part count — the fewest of 1..16 parts of <= 20 segments each — inside
                       // the compiled 16-line region (lines past the count are never touched)
     int cls_p = 0;    // 1: one part count per class (the fewest with <= 1/256 of its lines over 20 segments)
+    int d16 = 0;      // 1: an 8-B word per (slot, /16) in front of DIR-24-8 answers /16s of <= 3 runs (A | B | A, values
+                      // <= 15 bits) by itself; other /16s read their tbl24 word after it
 };
+
+// Does (slot, /16 hi) have at most three runs of the A | B | A shape with values <= 0x7FFF?
+bool d16_inline(const infw_dev_tables &t, uint32_t slot, uint32_t hi) {
+    uint32_t vals[4], nr = 0, prev = ~0u;
+    for (uint32_t x = 0; x < 256; x++) {
+        const uint64_t e = t.tbl24[((uint64_t)slot << 24) | hi << 8 | x];
+        uint32_t seg[3], ns = 0;
+        if (!(e & INFW_D24_GROUP)) seg[ns++] = (uint32_t)e;
+        else {
+            uint32_t last = ~0u;
+            for (uint32_t y = 0; y < 256; y++) {
+                const uint32_t v = infw_dir24_lookup(t, slot, hi << 16 | x << 8 | y);
+                if (v != last) {
+                    if (ns == 3) return false;
+                    seg[ns++] = last = v;
+                }
+            }
+        }
+        for (uint32_t k = 0; k < ns; k++) {
+            if (seg[k] == prev) continue;
+            if (nr == 3 || seg[k] > 0x7FFFu) return false;
+            vals[nr++] = prev = seg[k];
+        }
+    }
+    return nr < 3 || vals[0] == vals[2];
+}
 
 }  // namespace
 
@@ -135,7 +163,9 @@ int main(int argc, char **argv) {
                             {"list_minor", false, false, 0, 64, 64, 0, 0, 0, 2},
                             {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3},
                             {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1},
-                            {"clsP", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 1}};
+                            {"clsP", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 1},
+                            {"d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1}};
+    std::vector<int8_t> d16ok;  // per (slot, /16): -1 unknown, 0 tbl24, 1 inline
     // per-class part counts for clsP
     int cls_plog[INFW_NCLS];
     for (int c = 0; c < INFW_NCLS; c++) {
@@ -377,7 +407,15 @@ int main(int argc, char **argv) {
                 }
                 if (!lng) {
                     const uint64_t w = ((uint64_t)slot << 24) | (a32 >> 8);
-                    tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 8)};
+                    bool skip24 = false;
+                    if (V.d16) {
+                        if (d16ok.empty()) d16ok.assign((size_t)t.n_slots << 16, -1);
+                        int8_t &ok = d16ok[((size_t)slot << 16) | (a32 >> 16)];
+                        if (ok < 0) ok = d16_inline(t, (uint32_t)slot, a32 >> 16);
+                        tc[nt++] = {S_D16, 6 * kSpace + (((uint64_t)slot << 16) | (a32 >> 16)) * 8};
+                        skip24 = ok;
+                    }
+                    if (!skip24) tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 8)};
                     if (V.dense_short) {  // the longest <= /32 prefix covering a32 in this slot
                         uint64_t r = ~0ull;
                         for (int L = 32; L >= 0 && r == ~0ull; L--) {
@@ -388,7 +426,7 @@ int main(int argc, char **argv) {
                         tc[nt - 1].addr = 1 * kSpace + (r == ~0ull ? (1ull << 35) + w * 8 : r * 8);
                     }
                     const uint64_t e = t.tbl24[w];
-                    if ((e & INFW_D24_GROUP) && !(e & INFW_D24_INLINE)) {
+                    if (!skip24 && (e & INFW_D24_GROUP) && !(e & INFW_D24_INLINE)) {
                         const uint64_t w8 = ((uint64_t)(uint32_t)e << 8) | (a32 & 0xFFu);
                         tc[nt++] = {S_TBL8, 2 * kSpace + w8 * 4};
                     }
