@@ -53,6 +53,13 @@ __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t
 
 // kLean: the epoch has no compressed short table (DIR-24-8 or none), no overflowed IPv6 group and no
 // partial-ifindex prefix (infw_dev_tables.lean), so those paths are compiled out.
+// Does the /24 of address bits 16..23 x lie inside one run of the inline /16 word w?  Then the word's answer is
+// the whole /24's, the meaning of an LDS word-cache entry.
+__device__ __forceinline__ bool d16_whole24(uint64_t w, uint32_t x) {
+    const uint32_t b = (uint32_t)(w >> 30) & 0xFFFFu, e1 = ((uint32_t)(w >> 46) & 0xFFFFu) + 1u;  // runs start at b, e1
+    return !(((b & 0xFFu) && (b >> 8) == x) || ((e1 & 0xFFu) && (e1 >> 8) == x));
+}
+
 // kD16: the epoch has /16 words in front of DIR-24-8 (infw_tables.h); a /16 they answer needs no tbl24 word.
 template <bool kCache, int kLog, bool kLean = false, bool kD16 = false>
 __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
@@ -67,7 +74,11 @@ __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T
     if ((e >> 63) && (uint32_t)(e >> 31) == key) return (uint32_t)e & 0x7FFFFFFFu;
     if (kD16) {
         const uint64_t d = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
-        if (d & INFW_D16_INLINE) return infw_d16_value(d, a32 & 0xFFFFu);
+        if (d & INFW_D16_INLINE) {
+            const uint32_t v = infw_d16_value(d, a32 & 0xFFFFu);
+            if (d16_whole24(d, (a32 >> 8) & 0xFFu)) s_c24[idx] = 1ull << 63 | (unsigned long long)key << 31 | v;
+            return v;
+        }
     }
     const uint64_t w = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
     if (w & INFW_D24_GROUP) {
@@ -675,6 +686,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     if (needd) {
                         if (wd & INFW_D16_INLINE) {
                             sh = infw_d16_value(wd, a32 & 0xFFFFu);
+                            // a /24 inside one run of the word: its answer goes to the LDS word cache, like a
+                            // plain tbl24 word's (Zipf traffic keeps its head there)
+                            if (kCache && slot < 256 && d16_whole24(wd, (a32 >> 8) & 0xFFu))
+                                s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | sh;
                         } else {
                             need24 = true;
                             w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
@@ -1031,7 +1046,11 @@ extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     // with per-list part counts their LDS copy replaces another half of the word cache (2 x 80 KiB per CU)
-    if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean)
+    if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean && T->d16_on)  // /16 words (sparse short tables)
+        launch<768, 0, 0, false, 6, false, false, 10, 9, true, true, 2, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    else if (T->lean && T->d16_on && T->n_dt_pl != INFW_DT_PL_LISTS)
+        launch<768, 0, 0, false, 6, false, false, 11, 9, true, true, 2, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
+    else if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean)
         launch<768, 0, 0, false, 6, false, false, 10, 9, true, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
     else if (T->n_dt_pl == INFW_DT_PL_LISTS)
         launch<768, 0, 0, false, 6, false, false, 10, 9, false, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);

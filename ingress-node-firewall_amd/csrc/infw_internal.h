@@ -253,8 +253,9 @@ struct IncState {
 // The /16 word of (slot, address bits 0..15) from the DIR-24-8 image: inline when its runs fit, else 0.
 // *runs: 1 for a /16 of one answer throughout (either way).
 uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs = nullptr);
-// Decide whether the epoch gets /16 words (INFW_D16=0/1 forces) and build them.
-void build_d16(HostTables &h);
+// Decide whether the epoch gets /16 words (INFW_D16=0/1 forces) and build them; n_short_wide of the n_short
+// <= /32 prefixes are /20 or shorter.
+void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide);
 
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
 int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,

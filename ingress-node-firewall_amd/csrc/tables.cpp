@@ -1193,7 +1193,11 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.dxr_idx.clear();
         out.dxr_lines.clear();
     }
-    build_d16(out);
+    {
+        uint64_t n_wide = 0;  // <= /32 prefixes of /20 or shorter
+        for (const ShortEnt &e : shorts) n_wide += e.plen <= 20;
+        build_d16(out, shorts.size(), n_wide);
+    }
     if (out.dxr_idx.empty()) out.dxr_idx.push_back(INFW_DXR_DIRECT);
     if (out.dxr_lines.empty()) out.dxr_lines.push_back(infw_dt_line{});
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
@@ -1475,7 +1479,7 @@ uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *run
     return infw_d16_encode(v[0], v[1], st[1], nr == 3 ? st[2] - 1 : 0xFFFFu);
 }
 
-void build_d16(HostTables &h) {
+void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide) {
     h.d16_on = 0;
     h.d16_permille = 0;
     h.d16.clear();
@@ -1507,9 +1511,14 @@ void build_d16(HostTables &h) {
             inl += cnt[2 * s + 1];
         }
         h.d16_permille = structured ? (uint32_t)(inl * 1000 / structured) : 1000u;
-        // worth a word in front of DIR-24-8 when most /16s with structure inside are answered by it: a lookup that
-        // falls through reads both (one more dependent L2 round trip)
-        if (req == 1 || h.d16_permille >= 500) {
+        // Worth a word in front of DIR-24-8 when almost every /16 with structure inside is answered by it (a lookup
+        // that falls through reads both: one more dependent L2 round trip) and prefixes of /20 or shorter — spread
+        // over 2..16 lines of DIR-24-8 words each, where the /16 word is one — are common.  Measured on MI355X
+        // (profiles/r03j, r03l): configs[1] (927 permille, 29 % of prefixes <= /20) +13 %, configs[4] (928, 33 %)
+        // +10 %; configs[2]-shaped tables (BGP-like, 12 % <= /20) -2..-5 % at 100k / 300k prefixes (891 / 698
+        // permille) and -9 % at 1M (262); configs[4] at 1M (451) even.
+        const bool wide = n_short && n_short_wide * 5 >= n_short;
+        if (req == 1 || (h.d16_permille >= 800 && wide)) {
             h.d16 = std::move(d);
             h.d16_on = 1;
         }

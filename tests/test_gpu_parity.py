@@ -497,8 +497,9 @@ def _frames_run(clf, dbuf, lens, fifx, n, dev, plen=None, offs=None, stride=0):
     return res.cpu().numpy().view(np.uint32)[:n], ver.cpu().numpy()[:n], clf.stats_read_all()
 
 
-@pytest.mark.parametrize("short_table,v6_form", [("dir24", "std"), ("compressed", "std"), ("dxr", "b2")])
-def test_classify_frames_on_device(monkeypatch, short_table, v6_form):
+@pytest.mark.parametrize("short_table,v6_form,d16", [("dir24", "std", "1"), ("dir24", "std", "0"), ("compressed", "std", ""),
+                                                    ("dxr", "b2", "")])
+def test_classify_frames_on_device(monkeypatch, short_table, v6_form, d16):
     """§8f-3 classification straight from raw frames (infw_classify_frames: the tuple is built in the kernel from
     the staged header window): result words, verdicts and counters equal the oracle's on the same frames —
     header snapshots at a fixed stride (a ragged count), and variable-length real frames back to back with an
@@ -508,6 +509,8 @@ def test_classify_frames_on_device(monkeypatch, short_table, v6_form):
     from frames import frame, snapshots
     monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
     monkeypatch.setenv("INFW_V6_FORM", v6_form)
+    if d16:  # /16 words in front of DIR-24-8 forced on / off
+        monkeypatch.setenv("INFW_D16", d16)
     dev = torch.device("cuda", 0)
     for cfg, npre, ntpl in ((W.CFG2_MIXED_1M, 50000, 256), (W.CFG4_ADVERSARIAL, 20000, 64)):
         wl = W.Workload(cfg, n_prefixes=npre, n_templates=ntpl)

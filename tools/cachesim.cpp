@@ -12,6 +12,8 @@
 //   tbl24_u16   DIR-24-8 words of 2 bytes (no inline /24s)
 //   entry32     decision entries of 32 B, a list's classes packed in 128-B lines
 //   quartersQ / partsQxB   entry lines addressed by (list, class, value part)
+//   d16         an 8-B word per (slot, /16) in front of DIR-24-8 answering /16s of <= 3 runs (A | B | A) alone
+// CACHESIM_CFG / CACHESIM_PREFIXES / CACHESIM_TEMPLATES pick the workload and its table size.
 // Build + run: make cachesim   (tools/cachesim [n_packets])
 #include <stdio.h>
 #include <stdlib.h>
@@ -113,7 +115,9 @@ int main(int argc, char **argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (4u << 20);
     infw_wl *wl = nullptr;
     const int cfg = getenv("CACHESIM_CFG") ? atoi(getenv("CACHESIM_CFG")) : INFW_WL_CFG2_MIXED_1M;
-    if (infw_wl_create(&wl, cfg, 0x1F000000ull + cfg, 0, 0)) return 1;
+    const uint32_t npfx = getenv("CACHESIM_PREFIXES") ? (uint32_t)atoi(getenv("CACHESIM_PREFIXES")) : 0;
+    const uint32_t ntpl = getenv("CACHESIM_TEMPLATES") ? (uint32_t)atoi(getenv("CACHESIM_TEMPLATES")) : 0;
+    if (infw_wl_create(&wl, cfg, 0x1F000000ull + cfg, npfx, ntpl)) return 1;
     PendingMap m;
     m.max_entries = 1u << 22;
     const uint64_t ne = infw_wl_n_entries(wl);

@@ -5,7 +5,7 @@ set -u
 O=gpurun_out/r03j
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-  -k "d16 or parity_configs or compact_layout or incremental or commits_while or many_ifindexes or lds_cache or clustered" \
+  -k "d16 or classify_frames_on_device or parity_configs or compact_layout or incremental or commits_while or many_ifindexes or lds_cache or clustered" \
   > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
