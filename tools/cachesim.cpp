@@ -79,6 +79,11 @@ struct Variant {
     int adapt = 0;    // 1: per-(list, class) part count — the fewest of 1..16 parts of <= 20 segments each — inside
                       // the compiled 16-line region (lines past the count are never touched)
     int cls_p = 0;    // 1: one part count per class (the fewest with <= 1/256 of its lines over 20 segments)
+    int lp = 0;       // > 0: IPv6 groups placed in sets of lp 32-B slots (one per record) at lp_load slot load, linear
+    double lp_load = 0.8;  // probing over sets with a per-set overflow flag; a lookup reads its home set and walks
+                      // on only through flagged sets
+    int set4 = 0;     // 1: IPv6 groups in 128-B sets of four 32-B slots at 0.8 slot load (a group takes 1..3 slots
+                      // of its home set; the lookup reads the home set's line)
     int d16 = 0;      // 1: an 8-B word per (slot, /16) in front of DIR-24-8 answers /16s of <= 3 runs (A | B | A, values
                       // <= 15 bits) by itself; other /16s read their tbl24 word after it
 };
@@ -168,7 +173,49 @@ int main(int argc, char **argv) {
                             {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3},
                             {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1},
                             {"clsP", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 1},
-                            {"d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1}};
+                            {"d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 1},
+                            {"set4", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 0},
+                            {"set4_d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 1},
+                            {"lp2_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.8},
+                            {"lp2_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.6},
+                            {"lp4_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.8},
+                            {"lp4_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.6}};
+    struct LpTab {
+        uint64_t sets = 0;
+        std::vector<uint8_t> used, flag;
+        std::unordered_map<uint64_t, uint64_t> at;  // group -> set
+    };
+    std::unordered_map<std::string, LpTab> lptabs;
+    auto lp_build = [&](const Variant &V) -> LpTab & {
+        LpTab &L = lptabs[V.name];
+        if (L.sets) return L;
+        uint64_t slots = 0;
+        std::vector<std::pair<uint64_t, uint32_t>> g;  // group key, slots
+        for (const auto &b : h.btab)
+            if (b.tag) {
+                uint32_t k = b.n == INFW_BUCKET_OVERFLOW ? 1u : b.n;
+                if (k > (uint32_t)V.lp) k = 1;  // more records than a set holds: an overflow marker
+                g.push_back({(uint64_t)(b.tag - 1) << 32 | b.top, k});
+                slots += k;
+            }
+        L.sets = std::max<uint64_t>(1, (uint64_t)(slots / (V.lp * V.lp_load)) + 1);
+        L.used.assign(L.sets, 0);
+        L.flag.assign(L.sets, 0);
+        uint64_t far = 0;
+        for (const auto &x : g) {
+            uint64_t s0 = infw_bucket_hash((uint32_t)(x.first >> 32), (uint32_t)x.first) % L.sets, s = s0;
+            while (L.used[s] + x.second > (uint32_t)V.lp) {
+                L.flag[s] = 1;
+                s = (s + 1) % L.sets;
+            }
+            L.used[s] += x.second;
+            L.at[x.first] = s;
+            far += s != s0;
+        }
+        fprintf(stderr, "[lp %s] %zu groups, %llu slots, %llu sets, %.4f off home\n", V.name, g.size(),
+                (unsigned long long)slots, (unsigned long long)L.sets, (double)far / std::max<size_t>(g.size(), 1));
+        return L;
+    };
     std::vector<int8_t> d16ok;  // per (slot, /16): -1 unknown, 0 tbl24, 1 inline
     // per-class part counts for clsP
     int cls_plog[INFW_NCLS];
@@ -399,6 +446,23 @@ int main(int argc, char **argv) {
                 if (pk == INFW_PK_V6 && t.n_levels) {
                     const uint64_t bi = infw_bucket_hash((uint32_t)slot, a32) & t.bmask;  // first probe only
                     tc[nt++] = {S_BUCKET, 0 * kSpace + bi * 64};
+                    if (V.lp) {  // home set, then the flagged sets after it until the group's own
+                        LpTab &L = lp_build(V);
+                        const uint64_t gk = (uint64_t)slot << 32 | a32;
+                        auto it = L.at.find(gk);
+                        uint64_t s = infw_bucket_hash((uint32_t)slot, a32) % L.sets;
+                        const uint32_t sb = V.lp * 32;
+                        tc[nt - 1].addr = 8 * kSpace + s * sb;
+                        for (int hop = 0; hop < 3; hop++) {  // (at most 6 touches per packet in the model)
+                            if ((it != L.at.end() && it->second == s) || !L.flag[s]) break;
+                            s = (s + 1) % L.sets;
+                            tc[nt++] = {S_BUCKET, 8 * kSpace + s * sb};
+                        }
+                    }
+                    if (V.set4) {  // slots needed: one per record of every group (n_buckets groups, ~1.3 records each)
+                        const uint64_t sets = std::max<uint64_t>(1, (uint64_t)(h.n_buckets * 1.31 / (4 * 0.8)));
+                        tc[nt - 1].addr = 7 * kSpace + (infw_bucket_hash((uint32_t)slot, a32) % sets) * 128;
+                    }
                     if (V.cuckoo) {
                         const uint64_t gk = (uint64_t)slot << 32 | a32;
                         auto it = cuckoo_at.find(gk);
