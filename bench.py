@@ -136,6 +136,9 @@ def parse(argv=None):
                     help="TEST ONLY: no GPU, ranks walk the compiled host image over gloo (not a measurement)")
     ap.add_argument("--compile-per-rank", action="store_true",
                     help="every rank compiles the table itself instead of importing rank 0's image")
+    ap.add_argument("--key-order", choices=("shuffled", "workload"), default="shuffled",
+                    help="order of the table updates: seeded random like the reference's Go map range (default), "
+                         "or the generator's popularity order (same map either way)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 27, help="packets per GPU per step")
@@ -210,13 +213,17 @@ def share_tables(args, clf, wl, rank, world, use_dist, log):
     import mmap
     import torch.distributed as dist
     t0 = time.time()
+    # the reference loader updates keys in Go map order (loader.go:158-208), i.e. at random: list ids — and so
+    # where each list's decision lines sit — follow first-update order, and the generator lists prefixes in
+    # popularity order, which would place the hot lists together (--key-order workload)
+    order = wl.shuffled_order() if args.key_order == "shuffled" else None
     if not use_dist or world == 1 or args.compile_per_rank:
-        wl.load_into(clf)
+        wl.load_into(clf, order=order)
         clf.commit()
         return "compiled", time.time() - t0
     path = [None]
     if rank == 0:
-        wl.load_into(clf)
+        wl.load_into(clf, order=order)
         clf.commit()
         size = clf.export_size()
         # shared memory when it has room (a container's /dev/shm may be small), else the temp directory; the file
@@ -251,7 +258,7 @@ def share_tables(args, clf, wl, rank, world, use_dist, log):
     how = "compiled"
     if rank != 0:
         if path[0] is None:
-            wl.load_into(clf)
+            wl.load_into(clf, order=order)
             clf.commit()
         else:
             import ctypes as C
@@ -609,7 +616,8 @@ def run_rank(args):
             "packets_counted_in_stats": counted,
             "stats_digest": digest,
             "tables": {"device_bytes_per_image": info["device_bytes"], "images_per_gpu": 2,
-                       "dt_parts": info["dt_parts"], "setup_s": round(commit_s, 2), "rank0": how,
+                       "dt_parts": info["dt_parts"], "d16_words": bool(info["d16"]), "key_order": args.key_order,
+                       "setup_s": round(commit_s, 2), "rank0": how,
                        "compile_ms": round(info["compile_ms"], 1), "upload_ms": round(info["upload_ms"], 1),
                        # peak host RSS of rank 0 (table compile + workload); the others import its image
                        "host_peak_rss_gib": round(peak_rss_gib, 2)},

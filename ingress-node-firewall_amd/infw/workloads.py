@@ -61,10 +61,33 @@ class Workload:
         return np.ctypeslib.as_array((C.c_uint8 * (1200 * self.n_templates)).from_address(
             N.wl.infw_wl_templates(self._h))).copy()
 
-    def load_into(self, classifier, flags: int = N.BPF_ANY) -> int:
-        """Push every entry through the table-map update path (batched)."""
-        return classifier.update_batch_ptr(N.wl.infw_wl_keys(self._h), N.wl.infw_wl_templates(self._h),
-                                           N.wl.infw_wl_val_index(self._h), self.n_entries, flags)
+    def load_into(self, classifier, flags: int = N.BPF_ANY, order=None) -> int:
+        """Push every entry through the table-map update path (batched), in the workload's order or in `order`
+        (a permutation of the entry indices).  The generator lists prefixes in popularity order; the reference's
+        loader updates keys in Go map order (loader.go:158-208: a map range, i.e. random), which a shuffled
+        order reproduces — list ids are assigned in first-update order, so the order places the decision lines."""
+        if order is None:
+            return classifier.update_batch_ptr(N.wl.infw_wl_keys(self._h), N.wl.infw_wl_templates(self._h),
+                                               N.wl.infw_wl_val_index(self._h), self.n_entries, flags)
+        order = np.asarray(order, dtype=np.int64)
+        keys = np.ascontiguousarray(self.keys_bytes().reshape(-1, 24)[order])
+        vi = np.ascontiguousarray(self.val_index()[order])
+        return classifier.update_batch_ptr(keys.ctypes.data, N.wl.infw_wl_templates(self._h), vi.ctypes.data,
+                                           len(order), flags)
+
+    def shuffled_order(self, seed: int = 0x5EED) -> np.ndarray:
+        """The entries that survive a load in workload order — for every LPM entry (prefixLen, ifindex and the
+        first prefixLen - 32 address bits; host bits ignored) its last update, which also fixes the host bits the
+        map keeps — in a seeded random order.  Loading these gives the same map as load_into() without `order`."""
+        kb = self.keys_bytes().reshape(-1, 24)
+        plen = kb[:, 0:4].copy().view("<u4").ravel().astype(np.int64)
+        bits = np.clip(plen[:, None] - 32 - 8 * np.arange(16)[None, :], 0, 8)          # address bits kept per byte
+        mask = ((0xFF00 >> bits) & 0xFF).astype(np.uint8)
+        masked = np.concatenate([kb[:, :8], kb[:, 8:] & mask], axis=1)
+        rows = np.ascontiguousarray(masked).view(np.dtype((np.void, 24))).ravel()
+        _, last_rev = np.unique(rows[::-1], return_index=True)
+        last = (len(rows) - 1 - last_rev).astype(np.int64)
+        return np.random.default_rng(seed).permutation(last)
 
     def entries(self):
         """(key bytes[24], value bytes[1200]) pairs in update order."""

@@ -43,3 +43,27 @@ def test_uniform_sources_flattens_the_head():
     assert np.array_equal(z.keys_bytes(), u.keys_bytes())
     top = lambda wl: np.sort(np.unique(wl.tuples(0, 50000)[:, 0], return_counts=True)[1])[-2]  # [-1]: word 0 of non-IP
     assert top(z) > 20 * top(u)
+
+
+def test_shuffled_key_order_builds_the_same_map():
+    """bench.py's default table load (--key-order shuffled: the reference loader's Go map order, at random) keeps,
+    per LPM entry, its last update of the workload order — value and host bits — so the committed map and every
+    classification equal the workload-order load's; duplicate keys (configs[4]'s identical v4 / v6 /0 keys,
+    generator repeats, host-bit variants) are where a plain shuffle would differ."""
+    import infw
+    for cfg, kw in ((W.CFG4_ADVERSARIAL, dict(n_prefixes=20000, n_templates=64)),
+                    (W.CFG2_MIXED_1M, dict(n_prefixes=30000, n_templates=30000)), (W.CFG1_V4_10K, {})):
+        wl = W.Workload(cfg, **kw)
+        a = infw.Classifier(flags=infw.F_HOST_ONLY)
+        wl.load_into(a)
+        a.commit()
+        order = wl.shuffled_order()
+        assert len(order) < wl.n_entries and len(set(order.tolist())) == len(order)
+        assert not np.array_equal(np.sort(order), order)
+        b = infw.Classifier(flags=infw.F_HOST_ONLY)
+        wl.load_into(b, order=order)
+        b.commit()
+        assert sorted((bytes(k), bytes(v)) for k, v in a.iterate()) == sorted((bytes(k), bytes(v)) for k, v in b.iterate())
+        hdr, cap, pl, ifx = wl.frames(0, 30000)
+        tup = W.pack_frames(hdr, cap, pl, ifx)
+        assert np.array_equal(a.debug_walk(tup), b.debug_walk(tup)), cfg
