@@ -123,7 +123,8 @@ def usable_cores():
 
 def workload_key(cfg, templates, prefixes):
     """Names the workload a traffic / PMC summary belongs to (profiles/traffic_<key>.json)."""
-    return f"cfg{cfg}" + ("_distinct" if templates and templates >= (prefixes or 1000000) else "")
+    return (f"cfg{cfg}" + ("_distinct" if templates and templates >= (prefixes or 1000000) else "") +
+            (f"_p{prefixes}" if prefixes else ""))
 
 
 def parse(argv=None):

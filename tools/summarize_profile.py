@@ -34,6 +34,8 @@ def main():
         os.path.join(src, "kt.stdout")) else []
     line = json.loads(bl[-1]) if bl else {}
     key = line.get("config", {}).get("workload_key", "cfg2")
+    if os.environ.get("PROFILE_KEY"):  # a line profiled before bench.py named its table size in the key
+        key = os.environ["PROFILE_KEY"]
     layout = line.get("roofline", {}).get("layout", "standard")
     if line:
         n = line["config"]["packets_per_gpu_per_step"]
