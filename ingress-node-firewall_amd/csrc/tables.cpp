@@ -904,15 +904,18 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     reserve_slack(out.desc, (size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, inc);
     out.desc.assign((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_DESC_STRIDE, 0);
     // value parts per (list, class): the fewest that keep one table line per packet (choose_dt_plog2),
-    // within a budget for the entry lines of one image — 16 GiB by default (INFW_DT_BUDGET_MB): at 1M
-    // distinct 99-rule lists 16 parts take 7.2 GB per image and measured fastest of 1..16 parts
-    // (3.37 vs 3.58 ms at 1 part + leaves, profiles/r02b); INFW_DT_PARTS=1|2|4|8|16 forces one form
+    // within a budget for the entry lines of one image — 2 GiB by default (INFW_DT_BUDGET_MB).  At 1M
+    // distinct 99-rule lists 16 parts take 7.2 GB per image; with the keys loaded in random order (the
+    // reference loader's Go map order) the hot lists' lines spread over all of it and every dependent
+    // decision-line read pays for the span: 4 parts (1.8 GB, a leaf line for busy parts) 3.75 ms against
+    // 5.03 at 16 (profiles/r03r; round 2's 16-part choice, profiles/r02b, was measured with the keys in
+    // popularity order, where the hot lists sit together); INFW_DT_PARTS=1|2|4|8|16 forces one form
     {
         std::vector<const uint8_t *> vals;
         vals.reserve(list_of_vid.size());
         for (const auto &p : list_of_vid) vals.push_back(m.pool.vals[p.first].data());
         out.dt_plog2 = choose_dt_plog2(vals);
-        uint64_t budget = 16ull << 30;
+        uint64_t budget = 2ull << 30;
         if (const char *e = getenv("INFW_DT_BUDGET_MB")) budget = strtoull(e, nullptr, 10) << 20;
         while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > budget)
             out.dt_plog2--;

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--prefixes", type=int, default=0, help="table size (0 = config default)")
     ap.add_argument("--templates", type=int, default=0,
                     help="distinct rule lists (0 = config default; >= prefixes: one list per key)")
+    ap.add_argument("--key-order", choices=("workload", "shuffled"), default="workload",
+                    help="table update order (bench.py's default is shuffled)")
     ap.add_argument("--launch", action="store_true", help="variants are launch-time settings (one table image)")
     args = ap.parse_args()
     import torch
@@ -69,7 +71,7 @@ def main():
             continue
         with applied({} if args.launch else envs[v]):
             c = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
-            wl.load_into(c)
+            wl.load_into(c, order=wl.shuffled_order() if args.key_order == "shuffled" else None)
             c.commit()
         info = c.info()
         print(f"[ab] {v}: {info['device_bytes'] / 2**20:.0f} MiB, compile {info['compile_ms']:.0f} ms, "

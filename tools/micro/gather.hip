@@ -4,6 +4,7 @@
 // W-aligned record of a T-byte table.  Reports lookups/s and record bytes/s.
 //   hipcc --offload-arch=gfx950 -O3 tools/micro/gather.hip -o gather && ./gather
 #include <hip/hip_runtime.h>
+#include <string.h>
 #include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -100,11 +101,19 @@ int main(int argc, char **argv) {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int grid = cus * 4;
-    const uint64_t max_t = 1ull << 30;
+    // "bigspread": the same measurement over spans up to 12 GiB (configs[2]'s one-list-per-key tables span 10.6 GiB)
+    const bool big = argc > 1 && strcmp(argv[1], "bigspread") == 0;
+    const uint64_t max_t = big ? 12ull << 30 : 1ull << 30;
     uint32_t *tab, *out;
-    hipMalloc(&tab, max_t);
+    if (hipMalloc(&tab, max_t) != hipSuccess) return 1;
     hipMemset(tab, 1, max_t);
     hipMalloc(&out, (size_t)grid * 512 * 4);
+    if (big) {
+        for (uint64_t f : {64ull << 20, 1ull << 30})
+            for (uint64_t span : {1ull << 30, 2ull << 30, 4ull << 30, 8ull << 30, 12ull << 30})
+                run_spread(tab, f, span, out, grid, 64);
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 's') {  // "spread": same L2 footprint over a growing address span
         for (uint64_t f : {2ull << 20, 16ull << 20, 64ull << 20})
             for (uint64_t span : {(uint64_t)f, (uint64_t)128 << 20, (uint64_t)1 << 30})

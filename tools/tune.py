@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--variants", default="768:0:2,512:0:3,512:0:4,256:0:6,512:8:3")
+    ap.add_argument("--prefixes", type=int, default=0, help="table size (0 = config default)")
+    ap.add_argument("--templates", type=int, default=0, help="distinct rule lists (0 = config default)")
+    ap.add_argument("--key-order", choices=("workload", "shuffled"), default="workload",
+                    help="table update order (bench.py's default is shuffled)")
     ap.add_argument("--ablate", default="", help="comma list of INFW_ABLATE codes to time (0 = full kernel)")
     args = ap.parse_args()
     import torch
@@ -30,9 +34,9 @@ def main():
     from infw import workloads as W
     from infw.batch import SoaBatch
     dev = torch.device("cuda", 0)
-    wl = W.Workload(args.cfg)
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
-    wl.load_into(clf)
+    wl.load_into(clf, order=wl.shuffled_order() if args.key_order == "shuffled" else None)
     clf.commit()
     n = args.batch
     batch = SoaBatch.empty(n, dev)
