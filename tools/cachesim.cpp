@@ -216,7 +216,8 @@ int main(int argc, char **argv) {
                 (unsigned long long)slots, (unsigned long long)L.sets, (double)far / std::max<size_t>(g.size(), 1));
         return L;
     };
-    std::vector<int8_t> d16ok;  // per (slot, /16): -1 unknown, 0 tbl24, 1 inline
+    std::vector<int8_t> d16ok;
+    const uint64_t tbl24_bytes = getenv("CACHESIM_TBL24_BYTES") ? atoi(getenv("CACHESIM_TBL24_BYTES")) : 8;  // word size  // per (slot, /16): -1 unknown, 0 tbl24, 1 inline
     // per-class part counts for clsP
     int cls_plog[INFW_NCLS];
     for (int c = 0; c < INFW_NCLS; c++) {
@@ -429,7 +430,12 @@ int main(int argc, char **argv) {
         // and leaf lines get an L2 of their own instead of sharing it with the LPM lines
         const bool phases = getenv("CACHESIM_PHASES") && atoi(getenv("CACHESIM_PHASES"));
         std::vector<L2> l2b(phases ? 8 : 0, L2(4ull << 20));
-        uint64_t req[S_N] = {}, miss[S_N] = {};
+        uint64_t req[S_N] = {}, miss[S_N] = {}, mmiss[S_N] = {};
+        // CACHESIM_MALL=1: the 256-MB Infinity Cache behind the L2s (one shared LRU model, 128-B lines); with
+        // CACHESIM_MALL_STREAM=1 the tuple stream's lines (32 B per packet) pass through it too
+        const bool mall_on = getenv("CACHESIM_MALL") && atoi(getenv("CACHESIM_MALL"));
+        const bool mall_stream = getenv("CACHESIM_MALL_STREAM") && atoi(getenv("CACHESIM_MALL_STREAM"));
+        L2 mall(mall_on ? (256ull << 20) : 2048);
         for (uint64_t i = 0; i < n; i++) {
             const uint32_t *q = &tup[i * 8];
             int cls = 0;
@@ -483,7 +489,7 @@ int main(int argc, char **argv) {
                         tc[nt++] = {S_D16, 6 * kSpace + (((uint64_t)slot << 16) | (a32 >> 16)) * 8};
                         skip24 = ok;
                     }
-                    if (!skip24) tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : 8)};
+                    if (!skip24) tc[nt++] = {S_TBL24, 1 * kSpace + w * (V.tbl24_u16 ? 2 : tbl24_bytes)};
                     if (V.dense_short) {  // the longest <= /32 prefix covering a32 in this slot
                         uint64_t r = ~0ull;
                         for (int L = 32; L >= 0 && r == ~0ull; L--) {
@@ -569,6 +575,7 @@ int main(int argc, char **argv) {
                 }
             }
             L2 &c = l2[(i / 512) % 8];
+            if (mall_stream && (i & 3) == 0) mall.access(9 * kSpace + i * 32);
             for (int k = 0; k < nt; k++) {
                 req[tc[k].s]++;
                 L2 *cp = phases && (tc[k].s == S_ENTRY || tc[k].s == S_LEAF) ? &l2b[(i / 512) % 8] : &c;
@@ -590,7 +597,10 @@ int main(int argc, char **argv) {
                     cp = &l2[((hk * 0xD6E8FEB86659FD93ull) >> 61) & 7];
                 }
                 L2 &ck = *cp;
-                if (!ck.access(tc[k].addr)) miss[tc[k].s]++;
+                if (!ck.access(tc[k].addr)) {
+                    miss[tc[k].s]++;
+                    if (mall_on && !mall.access(tc[k].addr)) mmiss[tc[k].s]++;
+                }
             }
         }
         double tr = 0, tm = 0;
@@ -600,7 +610,17 @@ int main(int argc, char **argv) {
             tr += (double)req[s] / n;
             tm += (double)miss[s] / n;
         }
-        printf(", \"requests\": %.4f, \"misses\": %.4f}\n", tr, tm);
+        printf(", \"requests\": %.4f, \"misses\": %.4f", tr, tm);
+        if (mall_on) {
+            double tmm = 0;
+            printf(", \"mall_misses\": {");
+            for (int s = 0; s < S_N; s++) {
+                printf("%s\"%s\": %.4f", s ? ", " : "", kName[s], (double)mmiss[s] / n);
+                tmm += (double)mmiss[s] / n;
+            }
+            printf("}, \"mall_misses_total\": %.4f", tmm);
+        }
+        printf("}\n");
         fflush(stdout);
     }
     infw_wl_destroy(wl);
