@@ -17,6 +17,7 @@ run cfg4 --cfg 4 --no-cpu-baseline --steps 30
 run cfg4_1m --cfg 4 --prefixes 1000000 --no-cpu-baseline --steps 30
 run cfg2_uniform --uniform --no-cpu-baseline --steps 30
 run cfg2_distinct --templates 1000000 --no-cpu-baseline --steps 20
+run cfg2_distinct_popularity_order --templates 1000000 --key-order workload --no-cpu-baseline --steps 20
 run cfg2_frames --from-frames 128 --no-cpu-baseline --steps 20
 run cfg2_frames_fused --from-frames 128 --fused --no-cpu-baseline --steps 20
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
