@@ -179,7 +179,9 @@ int main(int argc, char **argv) {
                             {"lp2_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.8},
                             {"lp2_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.6},
                             {"lp4_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.8},
-                            {"lp4_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.6}};
+                            {"lp4_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.6},
+                            {"lp1_50", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 0.5},
+                            {"lp1_25", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 0.25}};
     struct LpTab {
         uint64_t sets = 0;
         std::vector<uint8_t> used, flag;
@@ -194,7 +196,8 @@ int main(int argc, char **argv) {
         for (const auto &b : h.btab)
             if (b.tag) {
                 uint32_t k = b.n == INFW_BUCKET_OVERFLOW ? 1u : b.n;
-                if (k > (uint32_t)V.lp) k = 1;  // more records than a set holds: an overflow marker
+                if (k > (uint32_t)V.lp) k = 1;  // more records than a set holds: an overflow marker (lp 1: one
+                                                // group per 64-B bucket, as today, at a higher load)
                 g.push_back({(uint64_t)(b.tag - 1) << 32 | b.top, k});
                 slots += k;
             }
@@ -457,7 +460,7 @@ int main(int argc, char **argv) {
                         const uint64_t gk = (uint64_t)slot << 32 | a32;
                         auto it = L.at.find(gk);
                         uint64_t s = infw_bucket_hash((uint32_t)slot, a32) % L.sets;
-                        const uint32_t sb = V.lp * 32;
+                        const uint32_t sb = V.lp == 1 ? 64 : V.lp * 32;
                         tc[nt - 1].addr = 8 * kSpace + s * sb;
                         for (int hop = 0; hop < 3; hop++) {  // (at most 6 touches per packet in the model)
                             if ((it != L.at.end() && it->second == s) || !L.flag[s]) break;
