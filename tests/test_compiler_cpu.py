@@ -301,6 +301,11 @@ def test_host_sanitizer_walk():
     r = subprocess.run([os.path.join(root, "ingress-node-firewall_amd", "build", "asan_walk")], cwd=root, env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+    # and with /16 words in front of DIR-24-8 forced on (built per compile, re-derived by every patched commit)
+    env = dict(os.environ, INFW_D16="1", ASAN_CHURN_ROUNDS="3")
+    r = subprocess.run([os.path.join(root, "ingress-node-firewall_amd", "build", "asan_walk")], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def test_many_ifindexes_host_walk():
