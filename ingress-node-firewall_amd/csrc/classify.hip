@@ -53,11 +53,21 @@ __device__ __forceinline__ uint32_t d24_value(const infw_dev_tables &T, uint64_t
 
 // kLean: the epoch has no compressed short table (DIR-24-8 or none), no overflowed IPv6 group and no
 // partial-ifindex prefix (infw_dev_tables.lean), so those paths are compiled out.
-// Does the /24 of address bits 16..23 x lie inside one run of the inline /16 word w?  Then the word's answer is
-// the whole /24's, the meaning of an LDS word-cache entry.
-__device__ __forceinline__ bool d16_whole24(uint64_t w, uint32_t x) {
-    const uint32_t b = (uint32_t)(w >> 30) & 0xFFFFu, e1 = ((uint32_t)(w >> 46) & 0xFFFFu) + 1u;  // runs start at b, e1
-    return !(((b & 0xFFu) && (b >> 8) == x) || ((e1 & 0xFFu) && (e1 >> 8) == x));
+// kD16: the LDS word cache holds /16 words instead of /24 answers: entry i = two 8-B halves {tag ^ C, half of
+// the word}, tag = slot << 16 | /16 with bit 31 set; a torn pair fails the tag check.
+constexpr uint32_t kD16C0 = 0x5bd1e995u, kD16C1 = 0x9e3779b9u;
+template <int kLog>
+__device__ __forceinline__ uint32_t d16c_idx(uint32_t key16) { return (key16 * 0x9E3779B1u) >> (32 - (kLog - 1)); }
+__device__ __forceinline__ bool d16c_get(const unsigned long long *s, uint32_t idx, uint32_t key16, uint64_t &w) {
+    const unsigned long long e0 = s[2 * idx], e1 = s[2 * idx + 1];
+    const uint32_t tag = key16 | 0x80000000u;
+    w = (e1 << 32) | (e0 & 0xFFFFFFFFull);
+    return (uint32_t)(e0 >> 32) == (tag ^ kD16C0) && (uint32_t)(e1 >> 32) == (tag ^ kD16C1);
+}
+__device__ __forceinline__ void d16c_put(unsigned long long *s, uint32_t idx, uint32_t key16, uint64_t w) {
+    const uint32_t tag = key16 | 0x80000000u;
+    s[2 * idx] = (unsigned long long)(tag ^ kD16C0) << 32 | (uint32_t)w;
+    s[2 * idx + 1] = (unsigned long long)(tag ^ kD16C1) << 32 | (uint32_t)(w >> 32);
 }
 
 // kD16: the epoch has /16 words in front of DIR-24-8 (infw_tables.h); a /16 they answer needs no tbl24 word.
@@ -68,18 +78,20 @@ __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T
         return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? (kD16 ? infw_d16_lookup(T, slot, a32) : infw_dir24_lookup(T, slot, a32))
                         : T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, slot, a32) : 0u)
                      : infw_short_lookup(T, slot, a32);
+    if (kD16) {  // the LDS cache holds /16 words: a cached or fetched inline word answers, else the tbl24 word
+        const uint32_t key16 = slot << 16 | a32 >> 16, di = d16c_idx<kLog>(key16);
+        uint64_t d;
+        if (!d16c_get(s_c24, di, key16, d)) {
+            d = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
+            d16c_put(s_c24, di, key16, d);
+        }
+        if (d & INFW_D16_INLINE) return infw_d16_value(d, a32 & 0xFFFFu);
+        return infw_dir24_lookup(T, slot, a32);
+    }
     const uint32_t key = slot << 24 | a32 >> 8;
     const uint32_t idx = (key * 0x9E3779B1u) >> (32 - kLog);
     const unsigned long long e = s_c24[idx];
     if ((e >> 63) && (uint32_t)(e >> 31) == key) return (uint32_t)e & 0x7FFFFFFFu;
-    if (kD16) {
-        const uint64_t d = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
-        if (d & INFW_D16_INLINE) {
-            const uint32_t v = infw_d16_value(d, a32 & 0xFFFFu);
-            if (d16_whole24(d, (a32 >> 8) & 0xFFu)) s_c24[idx] = 1ull << 63 | (unsigned long long)key << 31 | v;
-            return v;
-        }
-    }
     const uint64_t w = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
     if (w & INFW_D24_GROUP) {
         if (w & INFW_D24_INLINE) return infw_d24_inline(w, a32 & 0xFFu);
@@ -640,11 +652,26 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     const bool needx = !v6 && T.short_mode == INFW_SHORT_DXR;  // range form: index word in the round
                     uint32_t wx = 0;
                     uint32_t sh = 0;
+                    bool d16known = false;  // kD16: the LDS cache held this /16's word and it does not answer
+                    const uint32_t key16 = (uint32_t)slot << 16 | a32 >> 16;
+                    const uint32_t d16i = kD16 ? d16c_idx<kC24Log>(key16) : 0u;
                     if (kCache && need24 && slot < 256) {
-                        const unsigned long long e = s_c24[cidx];
-                        if ((e >> 63) && (uint32_t)(e >> 31) == key) {
-                            sh = (uint32_t)e & 0x7FFFFFFFu;
-                            need24 = false;
+                        if (kD16) {
+                            uint64_t dw;
+                            if (d16c_get(s_c24, d16i, key16, dw)) {
+                                if (dw & INFW_D16_INLINE) {
+                                    sh = infw_d16_value(dw, a32 & 0xFFFFu);
+                                    need24 = false;
+                                } else {
+                                    d16known = true;
+                                }
+                            }
+                        } else {
+                            const unsigned long long e = s_c24[cidx];
+                            if ((e >> 63) && (uint32_t)(e >> 31) == key) {
+                                sh = (uint32_t)e & 0x7FFFFFFFu;
+                                need24 = false;
+                            }
                         }
                     }
                     uint64_t w24 = 0, bi = 0;
@@ -669,7 +696,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     // /16 words (kD16): an IPv4 lane the LDS cache did not answer reads its /16 word in this round
                     // instead of the tbl24 word, and the tbl24 word only when the /16 word does not answer
-                    const bool needd = kD16 && need24;
+                    const bool needd = kD16 && need24 && !d16known;
                     uint64_t wd = 0;
                     if (needd) {
                         need24 = false;
@@ -684,12 +711,9 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         br0 = b[1];
                     }
                     if (needd) {
+                        if (kCache && slot < 256) d16c_put(s_c24, d16i, key16, wd);
                         if (wd & INFW_D16_INLINE) {
                             sh = infw_d16_value(wd, a32 & 0xFFFFu);
-                            // a /24 inside one run of the word: its answer goes to the LDS word cache, like a
-                            // plain tbl24 word's (Zipf traffic keeps its head there)
-                            if (kCache && slot < 256 && d16_whole24(wd, (a32 >> 8) & 0xFFu))
-                                s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | sh;
                         } else {
                             need24 = true;
                             w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
@@ -705,7 +729,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     }
                     if (need24) {
                         sh = d24_value(T, w24, a32);
-                        if (kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
+                        if (!kD16 && kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
                             s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
                     } else if (needx) {
                         if (wx & INFW_DXR_DIRECT) {
