@@ -1028,6 +1028,49 @@ def test_lds_cache_collisions():
     assert len(np.unique(want[want != 0])) > 100  # the groups really answer with different lists
 
 
+def test_lds_d16_cache_collisions(monkeypatch):
+    """The LDS cache of /16 words (the kD16 kernels, INFW_D16=1) under maximal contention: 48 /16s answered by
+    their /16 word (a /20 inside each) and 16 /16s that are not (five /24s of different lists each), all mapped to 2
+    entries of the cache, each prefix with its own rule list; lanes of one wave keep overwriting the same entries
+    with different /16s' words, so a torn pair or a mixed-up word would answer with another /16's list."""
+    import random
+    import struct
+    import orc
+    import goenc
+    from test_incremental_cpu import _packets_for
+    monkeypatch.setenv("INFW_D16", "1")
+    rng = random.Random(12)
+    idx_bits = 10  # the per-list-part-count shape: 2048 LDS words = 1024 /16-word entries
+    his = []
+    while len(his) < 64:
+        hi = rng.getrandbits(16)
+        if hi not in his and (((hi * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - idx_bits)) in (7, 600):  # slot 0: key = hi
+            his.append(hi)
+    ents, order = {}, 1
+    for j, hi in enumerate(his):
+        subs = [(20, rng.getrandbits(4) << 12)] if j < 48 else [(24, rng.getrandbits(8) << 8) for _ in range(5)]
+        for L, lo in subs:
+            val = goenc.make_value([{"order": order % 99 + 1, "protocol": "TCP", "ports": "1-60000", "action": "Allow"}])
+            order += 1
+            ents[struct.pack("<II", L + 32, 1) + ((hi << 16) | lo).to_bytes(4, "big") + bytes(12)] = val
+    clf = infw.Classifier(devices=[0], max_entries=len(ents) + 16)
+    m = orc.OracleMap(max_entries=len(ents) + 16)
+    for k, v in ents.items():
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    clf.commit()
+    assert clf.info()["d16"] == 1
+    hdr, cap, pl, ifx = _packets_for(list(ents), rng, 1200)
+    perm = np.random.default_rng(5).permutation(len(ifx))
+    hdr, cap, pl, ifx = hdr[perm], cap[perm], pl[perm], ifx[perm]
+    want, _, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    dev = torch.device("cuda", 0)
+    clf.stats_reset()
+    got, _ = gpu_run(clf, SoaBatch.from_tuples(W.pack_frames(hdr, cap, pl, ifx), dev), len(ifx))
+    assert np.array_equal(got, want)
+    assert np.array_equal(clf.stats_read_all(), wst)
+    assert len(np.unique(want[want != 0])) > 60
+
+
 def test_classify_host_batches():
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
