@@ -2,6 +2,7 @@
 #   make            -> ingress-node-firewall_amd/lib/libinfw.so          (product: C ABI + HIP kernels)
 #                      ingress-node-firewall_amd/lib/libinfw_workload.so (bench/test workload generator)
 #                      oracle/build/liborc.so                            (test-only CPU oracle)
+#                      ingress-node-firewall_amd/lib/libinfw_loader.so   (host side: C++ pkg/ebpf + pkg/metrics)
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CC       ?= gcc
@@ -17,7 +18,7 @@ LIB_SRCS := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 
-all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so
+all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so $(OUT)/libinfw_loader.so $(OBJ)/loader_test
 
 # classify.hip: the LDS counter atomics are issued by one lane or at per-lane addresses, where the atomic
 # optimizer's wave scan (mbcnt, ballot count, multiply) is pure overhead in the hot loop
@@ -44,6 +45,15 @@ $(OUT)/libinfw.so: $(LIB_OBJS)
 $(OUT)/libinfw_workload.so: $(OBJ)/workload.hip.o
 	@mkdir -p $(OUT)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $<
+
+# host side above the C ABI: the C++ form of pkg/ebpf IngNodeFwController + pkg/metrics (the reference's host
+# side is Go, absent here), and the driver tests/test_loader_cpp.py runs it through
+HOST := $(PKG)/host
+$(OUT)/libinfw_loader.so: $(HOST)/infw_loader.cpp $(HOST)/infw_loader.hpp include/infw.h $(OUT)/libinfw.so
+	$(CXX) -std=c++17 -O2 -fPIC -shared -Wall -Wextra -o $@ $(HOST)/infw_loader.cpp -L$(OUT) -linfw -Wl,-rpath,'$$ORIGIN'
+$(OBJ)/loader_test: tests/c/loader_test.cpp $(OUT)/libinfw_loader.so
+	@mkdir -p $(OBJ)
+	$(CXX) -std=c++17 -O2 -Wall -Wextra -o $@ tests/c/loader_test.cpp -L$(OUT) -linfw_loader -linfw -Wl,-rpath,'$$ORIGIN/../lib'
 
 oracle/build/liborc.so: oracle/infw_oracle.c oracle/infw_oracle.h
 	@mkdir -p oracle/build

@@ -1,0 +1,166 @@
+// loader_test.cpp — driver of the C++ host-side loader (ingress-node-firewall_amd/host/infw_loader.hpp) for
+// tests/test_loader_cpp.py: reads a sync script on stdin, runs it on a host-only context (no GPU), prints the map.
+//
+// Script lines (whitespace-separated; "-" is an absent string):
+//   ifindex <name> <idx>...        GetInterfaceIndices(name) (a bond lists several)
+//   invalid <name>                 IsValidInterfaceNameAndState(name) == false
+//   debug <value>                  ENABLE_EBPF_LPM_LOOKUP_DBG=<value> for the next controller
+//   maxentries <n>                 table capacity of the context (before the first sync)
+//   sync ... endsync               one IngressNodeFwRulesLoader call:
+//     iface <name>                   an interface of the map
+//     ruleset <cidr>...              an IngressNodeFirewallRules of it
+//     rule <order> <protocol> <ports> <icmp_type> <icmp_code> <action>
+//   reset                          ResetAll
+//   dump                           GetBPFMapContentForTest
+//   selftest                       AddUInt64 / go_atoi known answers
+// Output: "sync <rc> <purge errors>", "reset <rc>", "dump <n>" + "entry <key hex> <value hex>" lines in key order,
+// "ctor <rc>", "selftest ok|FAILED".
+#include <errno.h>
+#include <stdio.h>
+
+#include <iostream>
+#include <map>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../ingress-node-firewall_amd/host/infw_loader.hpp"
+
+using namespace infw::loader;
+
+static std::string hex(const uint8_t *p, size_t n) {
+    static const char *d = "0123456789abcdef";
+    std::string s(2 * n, '0');
+    for (size_t i = 0; i < n; i++) {
+        s[2 * i] = d[p[i] >> 4];
+        s[2 * i + 1] = d[p[i] & 15];
+    }
+    return s;
+}
+
+static bool selftest() {
+    bool ok = true;
+    ok &= AddUInt64(0, 5) == std::make_pair<uint64_t, bool>(5, true);
+    ok &= AddUInt64(UINT64_MAX, 1) == std::make_pair<uint64_t, bool>(0, false);
+    ok &= AddUInt64(1ull << 63, 1ull << 62) == std::make_pair<uint64_t, bool>((1ull << 63) + (1ull << 62), true);
+    int64_t v = 0;
+    ok &= go_atoi("1", &v) && v == 1;
+    ok &= go_atoi("+7", &v) && v == 7;
+    ok &= go_atoi("-1", &v) && v == -1;
+    ok &= go_atoi("007", &v) && v == 7;
+    ok &= go_atoi("-9223372036854775808", &v) && v == INT64_MIN;
+    for (const char *bad : {"", " 1", "1 ", "0x10", "1.0", "+", "9223372036854775808"}) ok &= !go_atoi(bad, &v);
+    return ok;
+}
+
+int main() {
+    std::map<std::string, std::vector<uint32_t>> ifmap;
+    std::set<std::string> invalid;
+    std::string debug_env;
+    bool has_debug = false;
+    uint32_t max_entries = 1u << 20;
+    infw_ctx *ctx = nullptr;
+    IngNodeFwController *ctl = nullptr;
+    auto ensure = [&]() {
+        if (ctl) return;
+        if (infw_create(&ctx, nullptr, 0, max_entries, INFW_F_HOST_ONLY)) {
+            printf("create failed: %s\n", infw_last_error());
+            exit(2);
+        }
+        int rc = 0;
+        ctl = new IngNodeFwController(
+            ctx,
+            [&](const std::string &name, std::vector<uint32_t> *ids) {
+                auto it = ifmap.find(name);
+                if (it == ifmap.end()) return -ENODEV;  // "failed to get interface" (interfaces.go)
+                *ids = it->second;
+                return 0;
+            },
+            [&](const std::string &name) { return !invalid.count(name); }, has_debug ? debug_env.c_str() : nullptr,
+            &rc);
+        printf("ctor %d\n", rc);
+    };
+    std::string line;
+    InterfaceRules cur;
+    bool in_sync = false;
+    while (std::getline(std::cin, line)) {
+        std::istringstream in(line);
+        std::string op;
+        if (!(in >> op) || op[0] == '#') continue;
+        auto opt = [](const std::string &s) { return s == "-" ? std::string() : s; };
+        if (op == "ifindex") {
+            std::string name;
+            uint32_t idx;
+            in >> name;
+            auto &v = ifmap[name];
+            v.clear();
+            while (in >> idx) v.push_back(idx);
+        } else if (op == "invalid") {
+            std::string name;
+            in >> name;
+            invalid.insert(name);
+        } else if (op == "debug") {
+            in >> debug_env;
+            has_debug = true;
+        } else if (op == "maxentries") {
+            in >> max_entries;
+        } else if (op == "sync") {
+            cur.clear();
+            in_sync = true;
+        } else if (op == "iface" && in_sync) {
+            std::string name;
+            in >> name;
+            cur.emplace_back(name, std::vector<IngressNodeFirewallRules>{});
+        } else if (op == "ruleset" && in_sync) {
+            IngressNodeFirewallRules rs;
+            std::string c;
+            while (in >> c) rs.source_cidrs.push_back(c);
+            cur.back().second.push_back(rs);
+        } else if (op == "rule" && in_sync) {
+            ProtocolRule r;
+            std::string proto, ports, action;
+            unsigned t = 0, c = 0;
+            in >> r.order >> proto >> ports >> t >> c >> action;
+            r.protocol = opt(proto);
+            if (ports != "-") r.ports = ports;
+            r.icmp_type = (uint8_t)t;
+            r.icmp_code = (uint8_t)c;
+            r.action = action;
+            cur.back().second.back().rules.push_back(r);
+        } else if (op == "endsync") {
+            ensure();
+            std::vector<int> errs;
+            const int rc = ctl->IngressNodeFwRulesLoader(cur, &errs);
+            printf("sync %d %zu\n", rc, errs.size());
+            in_sync = false;
+        } else if (op == "reset") {
+            ensure();
+            printf("reset %d\n", ctl->ResetAll());
+        } else if (op == "dump") {
+            ensure();
+            std::map<KeyBytes, rulesVal_st> m;
+            const int rc = ctl->GetBPFMapContentForTest(&m);
+            printf("dump %d %zu\n", rc, m.size());
+            for (const auto &kv : m)
+                printf("entry %s %s\n", hex(kv.first.data(), kv.first.size()).c_str(),
+                       hex(reinterpret_cast<const uint8_t *>(&kv.second), sizeof kv.second).c_str());
+        } else if (op == "metrics") {
+            ensure();
+            Metrics mt;
+            const int rc = UpdateMetrics(ctx, &mt);
+            printf("metrics %d %llu %llu %llu %llu\n", rc, (unsigned long long)mt.allow_total,
+                   (unsigned long long)mt.allow_bytes, (unsigned long long)mt.deny_total,
+                   (unsigned long long)mt.deny_bytes);
+        } else if (op == "selftest") {
+            printf("selftest %s\n", selftest() ? "ok" : "FAILED");
+        } else {
+            printf("bad line: %s\n", line.c_str());
+            return 3;
+        }
+        fflush(stdout);
+    }
+    delete ctl;
+    if (ctx) infw_destroy(ctx);
+    return 0;
+}

@@ -1,0 +1,143 @@
+"""The C++ host side above the C ABI (ingress-node-firewall_amd/host/infw_loader.hpp: pkg/ebpf IngNodeFwController
+and pkg/metrics in C++, the form a daemon links where the reference's Go is absent), driven through
+tests/c/loader_test.cpp on a host-only context.  Checked against the reference's own expectations (the key sets of
+ebpfsyncer_test.go:727-987) and, map content byte for byte, against the Python mirror (infw/controller.py) over
+the reference's sync sequences — which test_golden.py pins to the reference's verdicts."""
+import os
+import subprocess
+
+import pytest
+
+import goenc
+import infw
+from test_golden import load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "ingress-node-firewall_amd", "build", "loader_test")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def driver():
+    r = subprocess.run(["make", "-s", "-C", ROOT, os.path.relpath(DRIVER, ROOT)], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and os.path.exists(DRIVER), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def run(script: str):
+    r = subprocess.run([DRIVER], input=script, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out, dumps, syncs = r.stdout.splitlines(), [], []
+    i = 0
+    while i < len(out):
+        f = out[i].split()
+        if f[0] == "dump":
+            assert f[1] == "0"
+            n = int(f[2])
+            dumps.append({bytes.fromhex(e.split()[1]): bytes.fromhex(e.split()[2]) for e in out[i + 1:i + 1 + n]})
+            i += n
+        elif f[0] == "sync":
+            syncs.append((int(f[1]), int(f[2])))
+        i += 1
+    return r.stdout, dumps, syncs
+
+
+def sync_lines(rules_by_iface) -> str:
+    s = ["sync"]
+    for name, ents in (rules_by_iface or {}).items():
+        s.append(f"iface {name}")
+        for e in ents:
+            s.append("ruleset " + " ".join(e["source_cidrs"]))
+            for r in e["rules"]:
+                ports = r.get("ports")
+                s.append(f"rule {r['order']} {r.get('protocol') or '-'} {'-' if ports is None else ports} "
+                         f"{r.get('icmp_type', 0)} {r.get('icmp_code', 0)} {r.get('action', 'Allow')}")
+    s.append("endsync")
+    return "\n".join(s) + "\n"
+
+
+def py_rules(rules_by_iface):
+    return {name: [infw.IngressNodeFirewallRules(e["source_cidrs"], [infw.ProtocolRule(**r) for r in e["rules"]])
+                   for e in ents] for name, ents in (rules_by_iface or {}).items()}
+
+
+def test_known_answers():
+    """addUInt64 (statistics.go:170-180) and strconv.Atoi (ENABLE_EBPF_LPM_LOOKUP_DBG, loader.go:72-83)."""
+    out, _, _ = run("selftest\n")
+    assert "selftest ok" in out
+    out, _, _ = run("debug 1\nreset\n")
+    assert "ctor 0" in out
+    out, _, _ = run("debug yes\nreset\n")
+    assert "ctor -22" in out
+
+
+@pytest.mark.parametrize("doc_name", ["ref_ebpfsyncer_keys.json", "ref_ebpfsyncer_http.json"])
+def test_reference_sync_sequences(doc_name):
+    """TestVerifyBPFKeysAfterInterfaceIngressRulesUpdate / TestSyncInterfaceIngressRulesWithHTTP: after every
+    sync the C++ loader's map has the reference's expected keys (where the test states them) and exactly the
+    Python mirror's keys and 1200-B values."""
+    doc = load(doc_name)
+    script = "".join(f"ifindex {n} {i}\n" for n, i in doc["ifindex"].items())
+    c = infw.Classifier(flags=infw.F_HOST_ONLY)
+    ctl = infw.IngNodeFwController(c, if_indices=lambda name: [doc["ifindex"][name]])
+    want = []
+    for tc in doc["test_cases"]:
+        if tc["isDelete"]:
+            script += "reset\n"
+            ctl.reset_all()
+        else:
+            script += sync_lines(tc["rules"])
+            ctl.ingress_node_fw_rules_loader(py_rules(tc["rules"]))
+        script += "dump\n"
+        want.append({k: bytes(v) for k, v in ctl.get_bpf_map_content_for_test().items()})
+    out, dumps, syncs = run(script)
+    assert all(rc == 0 and errs == 0 for rc, errs in syncs), out[-2000:]
+    assert len(dumps) == len(doc["test_cases"])
+    for tc, got, exp in zip(doc["test_cases"], dumps, want):
+        assert got == exp, tc["name"]
+        if "expectedKeys" in tc:
+            assert set(got) == {goenc.build_key(doc["ifindex"][i], cidr) for i, cidr in tc["expectedKeys"]}, tc["name"]
+
+
+def test_e2e_table_and_invalid_interfaces():
+    """The e2e behavioural table's rule sets (e2e.go:176-831, merged per node as the operator does) including an
+    interface that does not exist — skipped as loader.go:143-146 does — equal the Python mirror's map."""
+    from e2e_ref import DOC
+    for case in DOC["cases"]:
+        rules = case["interface_ingress_rules"]
+        script = "".join(f"ifindex {n} {i}\n" for n, i in DOC["ifindex"].items())
+        script += "".join(f"invalid {n}\n" for n in rules if n not in DOC["ifindex"])
+        script += sync_lines(rules) + "dump\n"
+        c = infw.Classifier(flags=infw.F_HOST_ONLY)
+        ctl = infw.IngNodeFwController(c, if_indices=lambda name: [DOC["ifindex"][name]],
+                                       is_valid_interface=lambda name: name in DOC["ifindex"])
+        ctl.ingress_node_fw_rules_loader(py_rules(rules))
+        out, dumps, syncs = run(script)
+        assert syncs == [(0, 0)], out[-1000:]
+        assert dumps[0] == {k: bytes(v) for k, v in ctl.get_bpf_map_content_for_test().items()}, case["cite"]
+        assert dumps[0], case["cite"]
+
+
+def test_errors_like_the_go_loader():
+    """A rule the Go code rejects fails the whole load before the map is touched (loader.go:158-162); an update
+    that hits a full map (ENOSPC, loader.go:200-208) ends the load with the keys before it published; stale keys
+    of the previous sync are purged; a bond's slaves each get the keys (loader.go:149)."""
+    base = "ifindex eth0 7\nifindex bond0 8 9\n"
+    ok = {"eth0": [{"source_cidrs": ["10.0.0.0/8"], "rules": [{"order": 1, "protocol": "TCP", "ports": "80",
+                                                                "action": "Deny"}]}]}
+    bad = {"eth0": [{"source_cidrs": ["11.0.0.0/8"], "rules": [{"order": 1, "protocol": "TCP", "ports": "200-100",
+                                                                 "action": "Deny"}]}]}
+    out, dumps, syncs = run(base + sync_lines(ok) + sync_lines(bad) + "dump\n")
+    assert syncs[0] == (0, 0) and syncs[1][0] == -22
+    assert set(dumps[0]) == {goenc.build_key(7, "10.0.0.0/8")}
+    full = {"eth0": [{"source_cidrs": ["10.0.0.0/8", "11.0.0.0/8", "12.0.0.0/8"],
+                      "rules": [{"order": 1, "protocol": "TCP", "ports": "80", "action": "Deny"}]}]}
+    out, dumps, syncs = run("maxentries 2\n" + base + sync_lines(full) + "dump\n")
+    assert syncs[0][0] == -28 and len(dumps[0]) == 2   # ENOSPC; the two applied keys are committed
+    bond = {"bond0": [{"source_cidrs": ["1.1.1.0/24", "100:1::/64"], "rules": [{"order": 5, "protocol": "UDP",
+                                                                                 "ports": "53", "action": "Allow"}]}]}
+    out, dumps, syncs = run(base + sync_lines(ok) + sync_lines(bond) + "dump\n")
+    assert syncs == [(0, 0), (0, 0)]
+    assert set(dumps[0]) == {goenc.build_key(i, c) for i in (8, 9) for c in ("1.1.1.0/24", "100:1::/64")}
+    assert all(v == goenc.make_value(bond["bond0"][0]["rules"]) for v in dumps[0].values())
+    out, _, syncs = run(base + sync_lines({"ghost": ok["eth0"]}))
+    assert syncs[0][0] == -19   # GetInterfaceIndices fails: the load returns its error
