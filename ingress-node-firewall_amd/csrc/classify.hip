@@ -920,8 +920,10 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
         launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on)
         launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    // with per-list part counts (16 KiB of LDS) a 4096-entry word cache and a 256-entry IPv6 group cache: same-box
+    // alternating A/B against 2048 + 512 at configs[2], 2.361 vs 2.378 ms (profiles/r03zc)
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        launch<768, 0, 0, false, 6, false, kC, 12, 8, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)
         launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)

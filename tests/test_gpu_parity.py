@@ -990,7 +990,7 @@ def test_lds_cache_collisions():
     import orc
     from test_incremental_cpu import _packets_for
     rng = random.Random(11)
-    b6_log, c24_log = 9, 12  # the default shape's cache sizes (768 x 2)
+    b6_log, c24_log = 8, 12  # the default shape's cache sizes with per-list part counts (768 x 2, <= 4096 lists)
     want6 = {}
     while len(want6) < 64:
         top = rng.getrandbits(32)
