@@ -330,6 +330,31 @@ int main(int argc, char **argv) {
                (double)probes / looks, (double)wave_max_sum / waves, (double)h.n_buckets / h.btab.size(), hist[1],
                hist[2], hist[3], hist[4], hist[5], hist[6], hist[7]);
     }
+    for (int lds_entries : {512, 1024, 2048}) {  // per-workgroup LDS cache of first-match results keyed by
+        // (list, class, value): a hit needs no decision line (Zipf-hot lists with service ports repeat the key)
+        const uint64_t per_wg = getenv("CACHESIM_WG_PACKETS") ? strtoull(getenv("CACHESIM_WG_PACKETS"), 0, 10) : 131072;
+        const uint32_t wgs = (uint32_t)(n / per_wg) ? (uint32_t)(n / per_wg) : 1;
+        std::vector<uint64_t> tag((size_t)wgs * lds_entries, ~0ull);
+        uint64_t look = 0, hit = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t *q = &tup[i * 8];
+            int cls = 0;
+            uint32_t val = 0;
+            const int pk = infw_parse(q[6], q[7], &cls, &val);
+            if (pk < INFW_PK_V4) continue;
+            const uint32_t l1 = infw_lpm(t, pk, q[4], q);
+            if (!l1) continue;
+            const uint64_t key = (uint64_t)l1 << 19 | (uint64_t)cls << 16 | val;
+            const uint32_t wg = (uint32_t)((i / 768) % wgs);
+            const uint32_t idx = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) % (uint32_t)lds_entries;
+            uint64_t &e = tag[(size_t)wg * lds_entries + idx];
+            look++;
+            hit += e == key;
+            e = key;
+        }
+        printf("{\"lds_result_cache\": %d, \"decision_lookups_per_packet\": %.4f, \"hit_rate\": %.4f}\n", lds_entries,
+               (double)look / n, (double)hit / std::max<uint64_t>(look, 1));
+    }
     for (int lds_entries : {256, 1024, 2048}) {  // per-workgroup direct-mapped LDS cache of tbl24 words
         const uint64_t per_wg = getenv("CACHESIM_WG_PACKETS") ? strtoull(getenv("CACHESIM_WG_PACKETS"), 0, 10) : 131072;
         const uint32_t wgs = (uint32_t)(n / per_wg) ? (uint32_t)(n / per_wg) : 1;  // ~131k packets per workgroup, as at 128M packets over 1024 workgroups
