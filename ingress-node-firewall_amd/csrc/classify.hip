@@ -27,6 +27,9 @@
 namespace {
 
 constexpr int kStatKeys = INFW_MAX_TARGETS;
+// rule ids with a workgroup counter in LDS (the Go loader writes 1..99, loader.go:437); higher ids (< 1024) add
+// straight to the device counters
+constexpr int kLdsStatKeys = 128;
 constexpr uint32_t kBigLen = 1u << 20;                      // frames this long skip the packed LDS counters
 constexpr unsigned long long kBytesMask = (1ull << 40) - 1;  // bytes field of a packed LDS counter
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     // per-workgroup counters [rule][allow=0, deny=1], packets << 40 | bytes in one u64 (one LDS atomic per update):
     // only frames shorter than kBigLen take this path and the workgroup flushes every kFlushTiles tiles, so
     // neither field can carry into the other (kFlushTiles * kBlock * kBigLen < 2^40)
-    __shared__ unsigned long long s_c[2 * kStatKeys];
+    __shared__ unsigned long long s_c[2 * kLdsStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
     // diagnostic 32: no LDS word cache and no IPv6 group cache, 1024: no word cache only; the 256-thread shapes
     // (6 blocks per CU) have no LDS room for it
@@ -429,10 +432,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         for (uint32_t i = threadIdx.x; i < INFW_DT_PL_LISTS; i += kBlock) s_pl[i] = T.dt_pl[i];
     if (kB6)
         for (int i = threadIdx.x; i < (int)(2u << kB6Log); i += kBlock) s_b6[i] = u32x4{0u, 0u, 0u, 0u};
-    for (int i = threadIdx.x; i < 2 * kStatKeys; i += kBlock) s_c[i] = 0;
+    for (int i = threadIdx.x; i < 2 * kLdsStatKeys; i += kBlock) s_c[i] = 0;
     // the workgroup's counters -> the device's (one u64 atomic per touched counter), zeroed for the next tiles
     auto flush_counters = [&]() {
-        for (int s = threadIdx.x; s < 2 * kStatKeys; s += kBlock) {
+        for (int s = threadIdx.x; s < 2 * kLdsStatKeys; s += kBlock) {
             const unsigned long long c = s_c[s];
             if (c) {
                 unsigned long long *dst = stats + (s >> 1) * 4 + (s & 1) * 2;
@@ -824,13 +827,15 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             // counter slot of this packet, or -1 (no stats: UNDEF, action outside {1,2}, key >= 1024)
             const int s0_ = (valid && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
                                 ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
-            // a frame of kBigLen bytes or more (never a real frame) goes straight to the device counters
-            if (s0_ >= 0 && plen >= kBigLen) {
+            // a frame of kBigLen bytes or more (never a real frame), or a rule id without an LDS counter, goes
+            // straight to the device counters
+            const bool lds = plen < kBigLen && key < (uint32_t)kLdsStatKeys;
+            if (s0_ >= 0 && !lds) {
                 unsigned long long *dst = stats + (s0_ >> 1) * 4 + (s0_ & 1) * 2;
                 atomicAdd(dst, 1ull);
                 atomicAdd(dst + 1, (unsigned long long)plen);
             }
-            const int s = plen < kBigLen ? s0_ : -1;
+            const int s = lds ? s0_ : -1;
             // per-wavefront aggregation of the most common slot (Zipf traffic: the first eligible
             // lane's slot): its lanes are summed in registers and added once; the rest go to LDS
             const uint64_t elig = __ballot(s >= 0);
@@ -923,7 +928,7 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     // with per-list part counts (16 KiB of LDS) a 4096-entry word cache and a 256-entry IPv6 group cache: same-box
     // alternating A/B against 2048 + 512 at configs[2], 2.361 vs 2.378 ms (profiles/r03zc)
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, kC, 12, 8, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)
         launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)
