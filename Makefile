@@ -18,7 +18,7 @@ LIB_SRCS := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 
-all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so $(OUT)/libinfw_loader.so $(OBJ)/loader_test
+all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so $(OUT)/libinfw_loader.so $(OUT)/infw_loader_test
 
 # classify.hip: the LDS counter atomics are issued by one lane or at per-lane addresses, where the atomic
 # optimizer's wave scan (mbcnt, ballot count, multiply) is pure overhead in the hot loop
@@ -51,9 +51,9 @@ $(OUT)/libinfw_workload.so: $(OBJ)/workload.hip.o
 HOST := $(PKG)/host
 $(OUT)/libinfw_loader.so: $(HOST)/infw_loader.cpp $(HOST)/infw_loader.hpp include/infw.h $(OUT)/libinfw.so
 	$(CXX) -std=c++17 -O2 -fPIC -shared -Wall -Wextra -o $@ $(HOST)/infw_loader.cpp -L$(OUT) -linfw -Wl,-rpath,'$$ORIGIN'
-$(OBJ)/loader_test: tests/c/loader_test.cpp $(OUT)/libinfw_loader.so
-	@mkdir -p $(OBJ)
-	$(CXX) -std=c++17 -O2 -Wall -Wextra -o $@ tests/c/loader_test.cpp -L$(OUT) -linfw_loader -linfw -Wl,-rpath,'$$ORIGIN/../lib'
+# (in lib/, beside the libraries, so the GPU box gets the binary with them: tests/test_loader_cpp.py runs it there too)
+$(OUT)/infw_loader_test: tests/c/loader_test.cpp $(OUT)/libinfw_loader.so
+	$(CXX) -std=c++17 -O2 -Wall -Wextra -o $@ tests/c/loader_test.cpp -L$(OUT) -linfw_loader -linfw -Wl,-rpath,'$$ORIGIN'
 
 oracle/build/liborc.so: oracle/infw_oracle.c oracle/infw_oracle.h
 	@mkdir -p oracle/build

@@ -1,5 +1,5 @@
 // loader_test.cpp — driver of the C++ host-side loader (ingress-node-firewall_amd/host/infw_loader.hpp) for
-// tests/test_loader_cpp.py: reads a sync script on stdin, runs it on a host-only context (no GPU), prints the map.
+// tests/test_loader_cpp.py: reads a sync script on stdin, runs it on a context (host-only unless `device`), prints the map.
 //
 // Script lines (whitespace-separated; "-" is an absent string):
 //   ifindex <name> <idx>...        GetInterfaceIndices(name) (a bond lists several)
@@ -13,11 +13,17 @@
 //   reset                          ResetAll
 //   dump                           GetBPFMapContentForTest
 //   selftest                       AddUInt64 / go_atoi known answers
+//   device                         the context drives HIP device 0 (before the first sync; default: host-only)
+//   classify <file>                the tuples in <file> (n x 8 u32: saddr[4], ifindex, pkt_len, meta, l4word) through
+//                                  infw_classify_host on device 0; walk <file>: through the host image instead
+//   metrics                        UpdateMetrics (statistics.go:112-167) over the context's statistics slots
 // Output: "sync <rc> <purge errors>", "reset <rc>", "dump <n>" + "entry <key hex> <value hex>" lines in key order,
-// "ctor <rc>", "selftest ok|FAILED".
+// "ctor <rc>", "selftest ok|FAILED", "results <rc> <n>" + one hex result word per line, "metrics <rc> <4 totals>".
 #include <errno.h>
 #include <stdio.h>
+#include <string.h>
 
+#include <fstream>
 #include <iostream>
 #include <map>
 #include <set>
@@ -60,11 +66,14 @@ int main() {
     std::string debug_env;
     bool has_debug = false;
     uint32_t max_entries = 1u << 20;
+    bool on_device = false;
     infw_ctx *ctx = nullptr;
     IngNodeFwController *ctl = nullptr;
     auto ensure = [&]() {
         if (ctl) return;
-        if (infw_create(&ctx, nullptr, 0, max_entries, INFW_F_HOST_ONLY)) {
+        const int dev0 = 0;
+        if (on_device ? infw_create(&ctx, &dev0, 1, max_entries, 0)
+                      : infw_create(&ctx, nullptr, 0, max_entries, INFW_F_HOST_ONLY)) {
             printf("create failed: %s\n", infw_last_error());
             exit(2);
         }
@@ -152,6 +161,40 @@ int main() {
             printf("metrics %d %llu %llu %llu %llu\n", rc, (unsigned long long)mt.allow_total,
                    (unsigned long long)mt.allow_bytes, (unsigned long long)mt.deny_total,
                    (unsigned long long)mt.deny_bytes);
+        } else if (op == "device") {
+            on_device = true;
+        } else if (op == "classify" || op == "walk") {
+            ensure();
+            std::string path;
+            in >> path;
+            std::vector<uint32_t> tup;  // the bytes as u32 words
+            {
+                std::ifstream g(path, std::ios::binary | std::ios::ate);
+                const std::streamsize bytes = g.tellg();
+                g.seekg(0);
+                tup.resize((size_t)bytes / 4);
+                g.read(reinterpret_cast<char *>(tup.data()), bytes);
+            }
+            const uint64_t n = tup.size() / 8;
+            std::vector<uint32_t> res(n ? n : 1);
+            int rc;
+            if (op == "walk") {
+                rc = infw_debug_walk(ctx, tup.data(), n, res.data());
+            } else {  // the SoA streams of the batch (infw_batch_soa) from the tuples, in host memory
+                std::vector<uint8_t> sa(16 * (n ? n : 1));
+                std::vector<uint32_t> ifx(n ? n : 1), plen(n ? n : 1), meta(n ? n : 1), l4(n ? n : 1);
+                for (uint64_t i = 0; i < n; i++) {
+                    memcpy(&sa[16 * i], &tup[8 * i], 16);
+                    ifx[i] = tup[8 * i + 4];
+                    plen[i] = tup[8 * i + 5];
+                    meta[i] = tup[8 * i + 6];
+                    l4[i] = tup[8 * i + 7];
+                }
+                const infw_batch_soa b{sa.data(), ifx.data(), plen.data(), meta.data(), l4.data()};
+                rc = infw_classify_host(ctx, 0, &b, n, res.data(), nullptr, 0);
+            }
+            printf("results %d %llu\n", rc, (unsigned long long)n);
+            for (uint64_t i = 0; i < n && rc == 0; i++) printf("%x\n", res[i]);
         } else if (op == "selftest") {
             printf("selftest %s\n", selftest() ? "ok" : "FAILED");
         } else {
