@@ -33,6 +33,7 @@ def main():
                     help="distinct rule lists (0 = config default; >= prefixes: one list per key)")
     ap.add_argument("--key-order", choices=("workload", "shuffled"), default="workload",
                     help="table update order (bench.py's default is shuffled)")
+    ap.add_argument("--uniform", action="store_true", help="sources uniform over the prefixes (bench.py --uniform)")
     ap.add_argument("--launch", action="store_true", help="variants are launch-time settings (one table image)")
     args = ap.parse_args()
     import torch
@@ -41,6 +42,8 @@ def main():
     from infw.batch import SoaBatch
     dev = torch.device("cuda", 0)
     wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
+    if args.uniform:
+        wl.uniform_sources()
     n = args.batch
     batch = SoaBatch.empty(n, dev)
     wl.gen_device(batch, 0, 0)
