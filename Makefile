@@ -26,7 +26,10 @@ $(OBJ)/classify.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 
 # build id (infw_build_id()): a hash of the kernel / table-layout sources and the flags they are compiled with;
 # bench.py only attaches a profile's PMC figures to a line when the profile was taken on the same build id
-BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h
+# (and a table image is accepted only by a library of the same build id, so every source that defines the serialised
+# layout — image.cpp's field order, infw_internal.h's HostTables / IncState, incremental.cpp's state — is in it)
+BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
+                $(SRC)/image.cpp $(SRC)/infw_internal.h $(SRC)/incremental.cpp
 $(OBJ)/infw_build_id.h: $(BUILDID_SRCS) Makefile
 	@mkdir -p $(OBJ)
 	@printf '#define INFW_BUILD_ID "%s"\n' "$$( (cat $(BUILDID_SRCS); echo '$(HIPFLAGS) $(EXTRA) $(ARCH)') | sha256sum | cut -c1-16)" > $@.tmp
@@ -74,10 +77,33 @@ asan:
 	    tools/asan_walk.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp -o $(OBJ)/asan_walk
 	$(OBJ)/asan_walk
 
+# AddressSanitizer/UBSan builds of the whole host side (CPU only; the gfx950 kernels' objects are the product's, their
+# device code is not instrumented): libinfw.so's host sources, the C++ loader and its driver, and tools/asan_abi.cpp,
+# which drives the host-only paths of the C ABI (map edits, commits, key walks, debug walk, encoders, table image
+# export / import incl. corrupt images).  tests/test_compiler_cpu.py and tests/test_loader_cpp.py run them.
+ASAN_DIR   := $(OBJ)/asan
+ASAN_FLAGS := -std=c++17 -g -O1 -fPIC -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+              -fno-omit-frame-pointer -Iinclude -I$(OBJ) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
+ASAN_SRCS  := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp
+ASAN_OBJS  := $(patsubst $(SRC)/%,$(ASAN_DIR)/%.o,$(ASAN_SRCS))
+HIP_OBJS   := $(OBJ)/classify.hip.o $(OBJ)/pack.hip.o $(OBJ)/patch.hip.o
+$(ASAN_DIR)/%.o: $(SRC)/% $(HDRS) $(OBJ)/infw_build_id.h
+	@mkdir -p $(ASAN_DIR)
+	g++ $(ASAN_FLAGS) -c $< -o $@
+$(ASAN_DIR)/libinfw.so: $(ASAN_OBJS) $(HIP_OBJS)
+	g++ -shared -fsanitize=address,undefined -o $@ $^ -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+$(ASAN_DIR)/libinfw_loader.so: $(HOST)/infw_loader.cpp $(HOST)/infw_loader.hpp $(ASAN_DIR)/libinfw.so
+	g++ $(ASAN_FLAGS) -shared -o $@ $(HOST)/infw_loader.cpp -L$(ASAN_DIR) -linfw -Wl,-rpath,'$$ORIGIN'
+$(ASAN_DIR)/infw_loader_test: tests/c/loader_test.cpp $(ASAN_DIR)/libinfw_loader.so
+	g++ $(ASAN_FLAGS) -o $@ tests/c/loader_test.cpp -L$(ASAN_DIR) -linfw_loader -linfw -Wl,-rpath,'$$ORIGIN'
+$(ASAN_DIR)/asan_abi: tools/asan_abi.cpp $(ASAN_DIR)/libinfw.so
+	g++ $(ASAN_FLAGS) -o $@ tools/asan_abi.cpp -L$(ASAN_DIR) -linfw -Wl,-rpath,'$$ORIGIN'
+asan-host: $(ASAN_DIR)/asan_abi $(ASAN_DIR)/infw_loader_test
+
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build
 
-.PHONY: all clean resource-usage asm asan cachesim patch_bench
+.PHONY: all clean resource-usage asm asan asan-host cachesim patch_bench
 
 # host model of the L2 behaviour of the table walk (layout experiments; tools/cachesim.cpp)
 cachesim: $(OUT)/libinfw_workload.so

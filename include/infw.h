@@ -513,9 +513,13 @@ int infw_table_export(infw_ctx *ctx, void *buf, uint64_t cap, uint64_t *size);
 /* Install an exported epoch into a context whose map is empty: the entries    */
 /* become the committed set (get_next_key / lookup / later incremental commits */
 /* work as after a commit) and every device slot gets the image — no compile.  */
-/* -EBUSY: the context already holds entries or edits; -EINVAL: not an image  */
-/* of this library build (infw_build_id) or truncated; -ENOSPC: more entries   */
-/* than max_entries.                                                           */
+/* -EBUSY: the context holds entries or uncommitted edits (one whose entries   */
+/* were all removed and committed counts as empty); -EINVAL: not an image of  */
+/* this library build (infw_build_id), truncated, a payload that does not     */
+/* match the header's XXH64, or compiled tables that fail the structural      */
+/* checks (an index outside its buffer, a probe table without a free slot) —  */
+/* nothing is installed or uploaded then; -ENOSPC: more entries than          */
+/* max_entries.                                                               */
 int infw_table_import(infw_ctx *ctx, const void *buf, uint64_t size);
 
 #ifdef __cplusplus

@@ -9,8 +9,13 @@
 //   - the compiled host tables (HostTables: every buffer the devices get, plus the bookkeeping incremental commits
 //     patch: tbl8 group index, counts, the chosen forms);
 //   - the incremental-commit state (IncState).
-// Layout: little-endian; a header (magic, format, ABI version, build id, element sizes) and then length-prefixed
-// arrays.  An image is only accepted by a library of the same build id: the table layout is the compiler's.
+// Layout: little-endian; a header (magic, format, ABI version, build id, element sizes, XXH64 of the payload) and
+// then length-prefixed arrays.  An image is only accepted by a library of the same build id (the build id hashes
+// every source that defines the serialised layout: Makefile BUILDID_SRCS), when the payload hashes to the
+// header's value, and when the parsed tables pass check_tables: every index the kernel or the host walk follows
+// stays inside its buffer and every probe loop has an empty slot to stop at — an image torn in /dev/shm or written
+// by a faulty exporter is refused with -EINVAL before anything is installed or uploaded (the verifier gate of the
+// reference's load, pkg/ebpf/ingress_node_firewall_loader.go:85-93, plays that role for its maps).
 #include <errno.h>
 #include <string.h>
 
@@ -25,7 +30,53 @@ namespace infw {
 namespace {
 
 constexpr char kMagic[8] = {'I', 'N', 'F', 'W', 'I', 'M', 'G', '1'};
-constexpr uint32_t kFormat = 1;
+constexpr uint32_t kFormat = 2;  // 2: payload hash in the header
+
+// XXH64 (seed 0) of the payload, the published xxHash 64-bit algorithm — tests recompute it with the xxhash module.
+constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull, kP2 = 0xC2B2AE3D27D4EB4Full, kP3 = 0x165667B19E3779F9ull,
+                   kP4 = 0x85EBCA77C2B2AE63ull, kP5 = 0x27D4EB2F165667C5ull;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+inline uint32_t rd32(const uint8_t *p) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+inline uint64_t xxh_round(uint64_t acc, uint64_t in) { return rotl64(acc + in * kP2, 31) * kP1; }
+inline uint64_t xxh_merge(uint64_t acc, uint64_t v) { return (acc ^ xxh_round(0, v)) * kP1 + kP4; }
+uint64_t xxh64(const uint8_t *p, uint64_t len) {
+    const uint8_t *const end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = kP1 + kP2, v2 = kP2, v3 = 0, v4 = 0 - kP1;
+        for (const uint8_t *lim = end - 32; p <= lim; p += 32) {
+            v1 = xxh_round(v1, rd64(p));
+            v2 = xxh_round(v2, rd64(p + 8));
+            v3 = xxh_round(v3, rd64(p + 16));
+            v4 = xxh_round(v4, rd64(p + 24));
+        }
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xxh_merge(xxh_merge(xxh_merge(xxh_merge(h, v1), v2), v3), v4);
+    } else {
+        h = kP5;
+    }
+    h += len;
+    for (; p + 8 <= end; p += 8) h = rotl64(h ^ xxh_round(0, rd64(p)), 27) * kP1 + kP4;
+    if (p + 4 <= end) {
+        h = rotl64(h ^ (uint64_t)rd32(p) * kP1, 23) * kP2 + kP3;
+        p += 4;
+    }
+    for (; p < end; p++) h = rotl64(h ^ (uint64_t)*p * kP5, 11) * kP1;
+    h ^= h >> 33;
+    h *= kP2;
+    h ^= h >> 29;
+    h *= kP3;
+    return h ^ (h >> 32);
+}
 
 struct Writer {
     uint8_t *p;  // nullptr: count only
@@ -74,7 +125,9 @@ struct Header {
     uint32_t format, abi;
     char build_id[32];
     uint32_t sz_bnode, sz_long, sz_bucket, sz_line;
+    uint64_t payload_hash;  // XXH64 of every byte after the header
 };
+static_assert(sizeof(Header) == 72, "image header layout");
 
 Header make_header(const char *build_id) {
     Header h;
@@ -179,7 +232,181 @@ uint64_t write_image(const PendingMap &m, const HostTables &h, const IncState &i
     map_write(w, inc.list_of_vid);
     w.vec(inc.list_refs);
     w.pod(inc.dead_lists);
+    if (out) {
+        const uint64_t hv = xxh64(out + sizeof(Header), w.n - sizeof(Header));
+        memcpy(out + offsetof(Header, payload_hash), &hv, sizeof hv);
+    }
     return w.n;
+}
+
+// Structural checks of parsed tables (see the file comment): list+1 values <= n_lists, group / node / line /
+// record indices inside their buffers, sizes as the compiler lays them out, the counters the kernel's lean
+// instantiation is chosen from equal to what the tables hold, and the incremental-commit state's ids in range.
+bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std::string *why) {
+    auto bad = [&](const char *what) {
+        *why = std::string("corrupt table image: ") + what;
+        return false;
+    };
+    auto pow2 = [](uint64_t x) { return x && !(x & (x - 1)); };
+    const uint64_t L = h.n_lists;  // list+1 values run 1..L (0 = no entry)
+    const uint64_t per_list = (uint64_t)INFW_NCLS << h.dt_plog2;
+    // never-empty device buffers (the compiler keeps a placeholder element in each)
+    if (h.tbl24.empty() || h.tbl8.empty() || h.nodes.empty() || h.vpool.empty() || h.rules.empty() ||
+        h.dtl.empty() || h.dte.empty() || h.desc.empty() || h.wild.size() < 3 || h.dxr_idx.empty() ||
+        h.dxr_lines.empty() || h.d16.empty() || h.l16.empty())
+        return bad("empty table buffer");
+    // ifindex map
+    const uint64_t nif = h.if_keys.size();
+    if (nif != h.if_slot.size() || !pow2(nif) || nif > (1u << 30) || h.n_slots > nif) return bad("ifindex map size");
+    bool if_free = false;
+    for (uint32_t s : h.if_slot) {
+        if (s == INFW_IF_EMPTY) if_free = true;
+        else if (s >= h.n_slots) return bad("ifindex slot out of range");
+    }
+    if (h.if_mult) {
+        int lg = 0;
+        while ((1ull << lg) < nif) lg++;
+        if (h.if_shift < 32u - (uint32_t)lg || h.if_shift > 31u) return bad("ifindex placement shift");
+    } else if (!if_free) {
+        return bad("ifindex map without a free slot");
+    }
+    // rule lists: decision lines, part counts, ballot-mode descriptors
+    if (h.dt_plog2 > 4 || h.n_lists >= (1u << 25)) return bad("rule list count or part count");
+    if (h.dte.size() < std::max<uint64_t>(L, 1) * per_list || h.desc.size() < std::max<uint64_t>(L, 1) * INFW_DESC_STRIDE)
+        return bad("decision / descriptor table size");
+    if (!h.dt_pl.empty()) {
+        if (h.dt_pl.size() != INFW_DT_PL_LISTS) return bad("part-count table size");
+        for (uint32_t w : h.dt_pl)
+            for (int c = 0; c < INFW_NCLS; c++)
+                if (((w >> (3 * c)) & 7u) > h.dt_plog2) return bad("part count above the image's");
+    }
+    for (const infw_dt_line &l : h.dte)
+        if (l.w[0] & INFW_DT_ROOT) {
+            // the root selects leaf index + (keys below v); pad keys (0xFFFF) never count
+            uint64_t keys = 0;
+            for (int k = 1; k < 16; k++) {
+                keys += (l.w[k] & 0xFFFFu) != 0xFFFFu;
+                keys += (l.w[k] >> 16) != 0xFFFFu;
+            }
+            if ((uint64_t)(l.w[0] & INFW_DT_INDEX) + keys >= h.dtl.size()) return bad("decision root past the leaf lines");
+        }
+    for (uint64_t d : h.desc)
+        if ((uint64_t)(uint32_t)d + (d >> 32) > h.rules.size()) return bad("class-list descriptor past the rules");
+    // short table (<= 32 address bits)
+    auto d24_ok = [&](uint64_t w) {
+        if (!(w & INFW_D24_GROUP)) return (w >> 32) == 0 && w <= L;
+        if (!(w & INFW_D24_INLINE)) return (uint64_t)(uint32_t)w < h.n_tbl8_groups;
+        if (w & INFW_D24_ABA) return (w & INFW_D24_ABA_MAXV) <= L && ((w >> 22) & INFW_D24_ABA_MAXV) <= L;
+        return (w & INFW_D24_MAXV) <= L && ((w >> 15) & INFW_D24_MAXV) <= L && ((w >> 30) & INFW_D24_MAXV) <= L;
+    };
+    const bool dir24_image = h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_DXR;
+    if (h.short_mode > INFW_SHORT_DXR) return bad("short-table form");
+    if (dir24_image) {
+        if (h.n_slots == 0 || h.tbl24.size() != ((uint64_t)h.n_slots << 24)) return bad("DIR-24-8 size");
+        if (h.tbl8.size() % 256 || h.tbl8.size() < h.n_tbl8_groups * 256) return bad("tbl8 size");
+        for (uint64_t w : h.tbl24)
+            if (!d24_ok(w)) return bad("DIR-24-8 word");
+        for (uint32_t v : h.tbl8)
+            if (v > L) return bad("tbl8 value");
+        for (const auto &g : h.tbl8_of)
+            if (g.second >= h.n_tbl8_groups || (g.first >> 24) >= h.n_slots) return bad("tbl8 group index");
+    }
+    if (h.d16_on) {
+        if (h.short_mode != INFW_SHORT_DIR24 || h.d16.size() != ((uint64_t)h.n_slots << 16)) return bad("/16 words");
+        for (uint64_t w : h.d16)
+            if ((w & INFW_D16_INLINE) && ((w & 0x7FFFu) > L || ((w >> 15) & 0x7FFFu) > L)) return bad("/16 word value");
+    }
+    if (h.short_mode == INFW_SHORT_DXR) {
+        if (h.dxr_idx.size() != ((uint64_t)h.n_slots << 16)) return bad("range index size");
+        for (uint32_t w : h.dxr_idx)
+            if ((w & INFW_DXR_DIRECT) ? (w & ~INFW_DXR_DIRECT) > L : w >= h.dxr_lines.size()) return bad("range index word");
+        for (const infw_dt_line &l : h.dxr_lines)
+            for (uint32_t j = 5; j < 16; j++)
+                if (l.w[j] > L) return bad("range line value");
+    }
+    if (h.short_mode == INFW_SHORT_COMPRESSED) {
+        if (h.l16.size() != ((uint64_t)std::max<uint32_t>(h.n_slots, 1) << 16)) return bad("compressed short-table size");
+        // a first-level node's children may be nodes, a second-level node's may not; each node checked once per level
+        std::vector<uint8_t> seen(h.nodes.size(), 0);
+        std::vector<std::pair<uint32_t, int>> todo;
+        auto value_ok = [&](uint32_t v, int level) {
+            if (!(v & INFW_NODE_FLAG)) return v <= L;
+            const uint32_t i = v & ~INFW_NODE_FLAG;
+            if (level >= 2 || i >= h.nodes.size()) return false;
+            if (!(seen[i] & (1u << level))) {
+                seen[i] |= (uint8_t)(1u << level);
+                todo.emplace_back(i, level + 1);
+            }
+            return true;
+        };
+        for (uint32_t w : h.l16)
+            if (!value_ok(w, 0)) return bad("compressed short-table word");
+        while (!todo.empty()) {
+            const auto [i, level] = todo.back();
+            todo.pop_back();
+            const infw_bnode &n = h.nodes[i];
+            uint32_t runs = 0;
+            for (uint32_t b : n.bm) runs += (uint32_t)__builtin_popcount(b);
+            if (!(n.bm[0] & 1u) || n.nv == 0 || runs != n.nv) return bad("short-table node bitmap");
+            if (n.nv > INFW_NODE_INLINE && (uint64_t)n.base + n.nv > h.vpool.size()) return bad("short-table node values");
+            for (uint32_t k = 0; k < n.nv; k++)
+                if (!value_ok(n.nv <= INFW_NODE_INLINE ? n.v[k] : h.vpool[n.base + k], level)) return bad("short-table node value");
+        }
+    }
+    // prefixes shorter than the ifindex
+    if ((uint64_t)h.n_wild * 3 > h.wild.size()) return bad("partial-ifindex list size");
+    for (uint32_t i = 0; i < h.n_wild; i++)
+        if (h.wild[3 * i] > 31 || h.wild[3 * i + 2] > L) return bad("partial-ifindex entry");
+    // IPv6 long prefixes: levels, Waldvogel table, /32-group buckets
+    if (h.levels.size() > INFW_MAX_LEVELS) return bad("IPv6 level count");
+    for (size_t i = 0; i < h.levels.size(); i++)
+        if (h.levels[i] < 33 || h.levels[i] > 128 || (i && h.levels[i] <= h.levels[i - 1])) return bad("IPv6 levels");
+    if (!pow2(h.ltab.size())) return bad("long-table size");
+    bool l_free = false;
+    for (const infw_long_entry &e : h.ltab) {
+        l_free |= e.tag == 0;
+        if (e.bmp > L) return bad("long-table value");
+    }
+    if (!l_free) return bad("long table without a free entry");
+    auto rec_ok = [&](const infw_v6_rec &r) { return (r.meta & 0x1FFFFFFu) <= L && (r.meta >> 25) >= 1 && (r.meta >> 25) <= 96; };
+    uint64_t overflowed = 0;
+    if (h.b2n) {
+        if (h.btab.size() != h.b2n) return bad("IPv6 slot-form size");
+        const infw_v6_slot *s = reinterpret_cast<const infw_v6_slot *>(h.btab.data());
+        for (uint64_t i = 0; i < 2 * h.b2n; i++) {
+            if (!s[i].tag) continue;
+            const uint32_t nr = s[i].info & 0xFFu;
+            if (s[i].tag > h.n_slots || (nr != 1 && nr != 2 && nr != INFW_BUCKET_OVERFLOW) ||
+                (nr != INFW_BUCKET_OVERFLOW && !rec_ok(s[i].rec)))
+                return bad("IPv6 slot");
+            overflowed += nr == INFW_BUCKET_OVERFLOW;
+        }
+    } else {
+        if (!pow2(h.btab.size())) return bad("IPv6 bucket-table size");
+        bool b_free = false;
+        for (const infw_v6_bucket &b : h.btab) {
+            if (!b.tag) {
+                b_free = true;
+                continue;
+            }
+            if (b.tag > h.n_slots || (b.n > INFW_BUCKET_INLINE && b.n != INFW_BUCKET_OVERFLOW)) return bad("IPv6 bucket");
+            if (b.n == INFW_BUCKET_OVERFLOW) overflowed++;
+            else
+                for (uint32_t k = 0; k < b.n; k++)
+                    if (!rec_ok(b.rec[k])) return bad("IPv6 record");
+        }
+        if (!b_free) return bad("IPv6 bucket table without a free bucket");
+    }
+    if (overflowed != h.n_overflow_groups || (overflowed && h.levels.empty())) return bad("IPv6 overflow groups");
+    // incremental-commit state
+    if (inc.valid) {
+        if (inc.list_refs.size() != L) return bad("list reference counts");
+        for (const auto &p : inc.slot_of)
+            if (p.second >= h.n_slots) return bad("ifindex slot of the commit state");
+        for (const auto &p : inc.list_of_vid)
+            if (p.first >= n_vals || p.second >= L) return bad("value -> list map");
+    }
+    return true;
 }
 
 }  // namespace
@@ -206,6 +433,10 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
         hd.sz_line != want.sz_line) {
         *why = std::string("image of another build (") + std::string(hd.build_id, strnlen(hd.build_id, 32)) +
                ", this library is " + build_id + ")";
+        return -EINVAL;
+    }
+    if (xxh64(buf + sizeof(Header), size - sizeof(Header)) != hd.payload_hash) {
+        *why = "payload hash mismatch (torn or corrupted image)";
         return -EINVAL;
     }
     uint64_t nv = 0;
@@ -244,16 +475,18 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
         *why = r.ok ? "trailing bytes after the image" : "truncated image";
         return -EINVAL;
     }
-    return 0;
+    return check_tables(h, inc, nv, why) ? 0 : -EINVAL;
 }
 
 // The committed set as the importer's pending map: values interned in id order (distinct values, so each gets the
-// id it had), then the nodes with their ids, indexed as update() would.
+// id it had), then the nodes with their ids, indexed as update() would.  A context whose entries were all removed
+// and committed counts as empty: its leftover value pool and tombstones are dropped first.
 int PendingMap::install_committed(const ImageEntries &ent, std::string *why) {
-    if (!nodes.empty() || !pool.vals.empty() || !dirty_ids.empty()) {
-        *why = "the context already holds entries";
+    if (!nodes.empty() || !dirty_ids.empty()) {
+        *why = "the context already holds entries or uncommitted edits";
         return -EBUSY;
     }
+    clear();
     if (ent.nodes.size() > max_entries) {
         *why = "more entries than max_entries";
         return -ENOSPC;

@@ -184,7 +184,10 @@ int IngNodeFwController::ResetAll() {
         rc = infw_table_delete(ctx_, &k);
         if (rc) return rc;
     }
-    return infw_table_commit(ctx_);
+    rc = infw_table_commit(ctx_);
+    if (rc) return rc;
+    // resetAll closes the objects (ebpfsyncer.go:170), the statistics map with them: the next load counts from zero
+    return infw_stats_reset(ctx_);
 }
 
 std::pair<uint64_t, bool> AddUInt64(uint64_t a, uint64_t b) {
@@ -195,13 +198,18 @@ std::pair<uint64_t, bool> AddUInt64(uint64_t a, uint64_t b) {
 }
 
 int UpdateMetrics(infw_ctx *ctx, Metrics *out) {
+    if (!ctx || !out) return -EINVAL;
     *out = Metrics{};
     const int nd = infw_num_devices(ctx);
     std::vector<ruleStatistics_st> slots((size_t)(nd > 0 ? nd : 1));
     for (uint32_t rule = 1; rule < kMaxIngressRules; rule++) {  // statistics.go:126
         int n = 0;
         const int rc = infw_stats_read(ctx, rule, slots.data(), &n);
-        if (rc) return rc;
+        if (rc) {  // statistics.go:127-130 logs the failed lookup and goes on with the next rule
+            out->failed_lookups++;
+            out->last_error = rc;
+            continue;
+        }
         for (int s = 0; s < n; s++) {  // a sum that wraps is dropped, as addUInt64's callers do (:135-156)
             auto add = [](uint64_t &acc, uint64_t v) {
                 const auto r = AddUInt64(v, acc);

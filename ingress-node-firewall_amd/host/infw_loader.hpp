@@ -94,8 +94,11 @@ std::pair<uint64_t, bool> AddUInt64(uint64_t a, uint64_t b);
 
 struct Metrics {
     uint64_t allow_total = 0, allow_bytes = 0, deny_total = 0, deny_bytes = 0;
+    uint32_t failed_lookups = 0;  // rules whose statistics read failed (skipped, as statistics.go:127-130 does)
+    int last_error = 0;           // the last such read's errno (negative)
 };
-// statistics.go:112-167: rules 1..MAX_INGRESS_RULES-1, every slot (one per device, like one per CPU).
+// statistics.go:112-167: rules 1..MAX_INGRESS_RULES-1, every slot (one per device, like one per CPU).  A failed read
+// of one rule is counted in failed_lookups and skipped; -EINVAL only for a null context or output.
 int UpdateMetrics(infw_ctx *ctx, Metrics *out);
 
 }  // namespace loader

@@ -21,7 +21,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Union
 
 from . import _native as N
 from .core import Classifier, build_ebpf_key
-from ._native import LpmIpKeySt, RulesValSt
+from ._native import InfwError, LpmIpKeySt, RulesValSt
 
 
 @dataclass
@@ -132,6 +132,7 @@ class IngNodeFwController:
         for k, _ in list(self.c.iterate()):
             self.c.delete(k)
         self.c.commit()
+        self.c.stats_reset()  # the statistics map goes with the closed objects (ebpfsyncer.go:170)
 
 
 def add_uint64(a: int, b: int):
@@ -154,8 +155,14 @@ class Statistics:
 
     def update_metrics(self) -> Dict[str, int]:
         allow = allow_b = deny = deny_b = 0
+        self.failed_lookups = 0
         for rule in range(1, self.MAX_INGRESS_RULES):        # statistics.go:126
-            for s in self.c.stats_read(rule):
+            try:
+                slots = self.c.stats_read(rule)
+            except InfwError:                                # statistics.go:127-130: logged, next rule
+                self.failed_lookups += 1
+                continue
+            for s in slots:
                 v, ok = add_uint64(s.allow_packets, allow)
                 allow = v if ok else allow
                 v, ok = add_uint64(s.allow_bytes, allow_b)

@@ -18,7 +18,7 @@
 //                                  infw_classify_host on device 0; walk <file>: through the host image instead
 //   metrics                        UpdateMetrics (statistics.go:112-167) over the context's statistics slots
 // Output: "sync <rc> <purge errors>", "reset <rc>", "dump <n>" + "entry <key hex> <value hex>" lines in key order,
-// "ctor <rc>", "selftest ok|FAILED", "results <rc> <n>" + one hex result word per line, "metrics <rc> <4 totals>".
+// "ctor <rc>", "selftest ok|FAILED", "results <rc> <n>" + one hex result word per line, "metrics <rc> <4 totals> <failed rule reads>".
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
@@ -158,9 +158,9 @@ int main() {
             ensure();
             Metrics mt;
             const int rc = UpdateMetrics(ctx, &mt);
-            printf("metrics %d %llu %llu %llu %llu\n", rc, (unsigned long long)mt.allow_total,
+            printf("metrics %d %llu %llu %llu %llu %u\n", rc, (unsigned long long)mt.allow_total,
                    (unsigned long long)mt.allow_bytes, (unsigned long long)mt.deny_total,
-                   (unsigned long long)mt.deny_bytes);
+                   (unsigned long long)mt.deny_bytes, mt.failed_lookups);
         } else if (op == "device") {
             on_device = true;
         } else if (op == "classify" || op == "walk") {

@@ -201,3 +201,6 @@ def test_e2e_metrics_on_device():
     m = infw.Statistics(clf).update_metrics()
     assert m["ingressnodefirewall_node_packet_deny_total"] == doc["expect"]["ingressnodefirewall_node_packet_deny_total"]
     assert m["ingressnodefirewall_node_packet_allow_total"] == 0
+    # resetAll drops the statistics map with the objects (ebpfsyncer.go:170): the next poll reads zero
+    ctl.reset_all()
+    assert all(v == 0 for v in infw.Statistics(clf).update_metrics().values())
