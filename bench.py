@@ -155,6 +155,8 @@ def parse(argv=None):
                     help="packets in the CPU-baseline sample (0: ~10-20 s of oracle work on the usable cores)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: every usable core)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-line-rates", action="store_true",
+                    help="skip the in-process random-line / stream rate probe (and so random_line_model)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (default profiles/traffic_<workload>.json when it matches the kernel)")
     ap.add_argument("--layout", default="standard", choices=["compact", "standard"],
@@ -450,6 +452,9 @@ def run_rank(args):
         args.layout = "frames"
         algo_bytes = 27 + 12 * n6 / max(n, 1)  # frame bytes kernel.c reads (11 B IPv4, 23 B IPv6) + 12 B lengths/ifindex + result
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
+    # the device's random-line and stream rates, measured in this process just before the timed loop (same lease,
+    # same device): what random_line_model prices the kernel's PMC line counts with (~0.3 s, untimed)
+    rates = None if args.no_line_rates else W.line_rates(local)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
@@ -564,16 +569,24 @@ def run_rank(args):
             traffic = None if traffic is None else round(traffic * n)
             traffic_from = (f"profiles/{tj.get('tag')}/summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {wkey}, "
                             f"build {tj.get('build_id')})")
-            # random-line model: the kernel's PMC L2 hits/misses per packet priced at the
-            # chip's measured random-lookup rates; frac = that bound / the measured kernel time
-            r = tj.get("line_rates")
-            if r and "l2_hits_per_packet" in tj:
+            # random-line model: the kernel's PMC L2 hits and misses per packet (the profile of this
+            # build) priced at the rates this process measured on this device before the timed loop: table hits at
+            # the L2-hit rate, table misses at the random-miss rate, and the streamed bytes (tuples in, result words
+            # out; for raw frames each frame's whole 128-B line) at the stream bandwidth — the stream's own lines
+            # are taken out of the L2 misses, not priced as random misses.  frac = that bound / the kernel time.
+            if rates and "l2_hits_per_packet" in tj:
                 h, m = tj["l2_hits_per_packet"], tj["l2_misses_per_packet"]
-                bound_ms = n * (h / (r["l2_hit_G_per_s"] * 1e9) + m / (r["l2_miss_G_per_s"] * 1e9)) * 1e3
+                stream_in = {"standard": 32.0, "compact": algo_bytes - 4, "frames": 12.0 + 128.0}[args.layout]
+                s_lines = (12.0 / 128 + 1.0) if args.layout == "frames" else stream_in / 128
+                tm = max(0.0, m - s_lines)
+                per_pkt_s = (h / (rates["l2_hit_G_per_s"] * 1e9) + tm / (rates["l2_miss_G_per_s"] * 1e9) +
+                             (stream_in + 4) / (rates["stream_GB_per_s"] * 1e9))
+                bound_ms = n * per_pkt_s * 1e3
                 line_model = {"l2_hits_per_packet": round(h, 3), "l2_misses_per_packet": round(m, 3),
-                              "hit_rate_G_per_s": r["l2_hit_G_per_s"], "miss_rate_G_per_s": r["l2_miss_G_per_s"],
+                              "stream_lines_per_packet": round(s_lines, 3), "table_misses_per_packet": round(tm, 3),
+                              "stream_bytes_per_packet": round(stream_in + 4, 2),
                               "bound_ms": round(bound_ms, 3), "frac": round(bound_ms / avg_kern_ms, 3),
-                              "counters_from": tj.get("tag")}
+                              "counters_from": tj.get("tag"), "rates": "line_rates (this process, same device)"}
             # SURVEY.md §8d's side figures: fabric-side line traffic (one TCC_EA0_RDREQ per 128-B line, stream and
             # gathers alike) as GB/s at this run's kernel time, and the LDS bank-conflict rate
             if "ea_rdreq_per_packet" in tj:
@@ -642,6 +655,7 @@ def run_rank(args):
             "algorithmic_bytes_per_packet": round(algo_bytes, 3),
             "layout": args.layout,
             "random_line_model": line_model,
+            "line_rates": rates,
             **extra,
             **extra_pipe,
         },

@@ -333,9 +333,88 @@ __global__ void gen_frames_kernel(infw_gen_params p, uint64_t start, uint64_t n,
     }
 }
 
+// ---- random-line and stream rates of the device, measured inside the bench's own process just before its timed
+// loop (bench.py random_line_model; tools/micro/gather.hip is the standalone microbenchmark they come from): the
+// rate of independent random 16-B lookups that hit the L2 (a 1-MiB table), of ones that miss it (a 2-GiB table:
+// every lookup a distinct line beyond the XCD L2s and the 256-MB Infinity Cache), and the read bandwidth of a
+// coalesced stream of 16-B non-temporal loads (the tuple stream's access pattern) over the same 2 GiB.
+typedef unsigned int lr_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lr_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    return x ^ (x >> 16);
+}
+__global__ __launch_bounds__(512) void lr_gather(const lr_u32x4 *__restrict__ tab, uint32_t mask, int iters,
+                                                 uint32_t *__restrict__ out) {
+    const uint32_t tid = blockIdx.x * 512 + threadIdx.x;
+    uint32_t acc = 0;
+    const uint32_t idx = lr_mix(tid);
+    for (int it = 0; it < iters; it++) {
+        const lr_u32x4 v = tab[lr_mix(idx + (uint32_t)it * 0x9E3779B9u) & mask];
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    out[tid] = acc;
+}
+__global__ __launch_bounds__(512) void lr_stream(const lr_u32x4 *__restrict__ buf, uint64_t n16, uint32_t *__restrict__ out) {
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 512 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 512) {
+        const lr_u32x4 v = __builtin_nontemporal_load(buf + i);
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// out[0] L2-hit lookups G/s, out[1] L2-miss lookups G/s, out[2] streamed read GB/s (device `dev`; ~0.3 s, 2 GiB of
+// scratch freed before returning).
+int infw_wl_line_rates(int dev, double *out) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (!out || hipSetDevice(dev) != hipSuccess) return -ENODEV;
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t grid = (uint32_t)(cus > 0 ? cus : 256) * 4;
+    const uint64_t big = 2ull << 30;
+    lr_u32x4 *tab = nullptr;
+    uint32_t *sink = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+    int rc = 0;
+    if (hipMalloc(&tab, big) != hipSuccess || hipMalloc(&sink, (size_t)grid * 512 * 4) != hipSuccess ||
+        hipMemset(tab, 1, big) != hipSuccess || hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+        rc = -ENOMEM;
+    auto timed = [&](auto launch, int reps) -> double {  // ms per launch after one untimed launch
+        launch();
+        (void)hipEventRecord(a, 0);
+        for (int r = 0; r < reps; r++) launch();
+        (void)hipEventRecord(b, 0);
+        (void)hipEventSynchronize(b);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, a, b);
+        return ms / reps;
+    };
+    const int iters = 64;
+    if (!rc) {
+        const double lookups = (double)grid * 512 * iters;
+        const double hit_ms = timed([&] { lr_gather<<<grid, 512>>>(tab, (1u << 20) / 16 - 1, iters, sink); }, 10);
+        const double miss_ms = timed([&] { lr_gather<<<grid, 512>>>(tab, (uint32_t)(big / 16 - 1), iters, sink); }, 5);
+        const double st_ms = timed([&] { lr_stream<<<grid * 2, 512>>>(tab, big / 16, sink); }, 5);
+        out[0] = lookups / (hit_ms * 1e-3) / 1e9;
+        out[1] = lookups / (miss_ms * 1e-3) / 1e9;
+        out[2] = (double)big / (st_ms * 1e-3) / 1e9;
+        if (hipGetLastError() != hipSuccess) rc = -EIO;
+    }
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    if (tab) (void)hipFree(tab);
+    if (sink) (void)hipFree(sink);
+    (void)hipSetDevice(prev);
+    return rc;
+}
 
 int infw_wl_create(infw_wl **out, int cfg, uint64_t seed, uint32_t n_prefixes, uint32_t n_templates) {
     if (!out) return -EINVAL;

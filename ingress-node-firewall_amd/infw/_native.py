@@ -259,6 +259,7 @@ wl = _load(WL_LIB_PATH)
 _wsig = {
     "infw_wl_create": (C.c_int, [P(C.c_void_p), C.c_int, C.c_uint64, C.c_uint32, C.c_uint32]),
     "infw_wl_destroy": (None, [C.c_void_p]),
+    "infw_wl_line_rates": (C.c_int, [C.c_int, P(C.c_double)]),
     "infw_wl_n_entries": (C.c_uint64, [C.c_void_p]),
     "infw_wl_keys": (C.c_void_p, [C.c_void_p]),
     "infw_wl_val_index": (C.c_void_p, [C.c_void_p]),

@@ -161,3 +161,12 @@ def pack_frames(hdr: np.ndarray, caplen: np.ndarray, pkt_len: np.ndarray, ifinde
     N.check(N.wl.infw_wl_pack(h.ctypes.data, cap.ctypes.data, pl.ctypes.data, ifx.ctypes.data, n, t.ctypes.data),
             "pack")
     return t
+
+
+def line_rates(dev_ordinal: int) -> dict:
+    """The device's random-line and stream rates measured now, in this process (infw_wl_line_rates, ~0.3 s):
+    independent random 16-B lookups hitting the L2 (1-MiB table) and missing it (2-GiB table), and coalesced
+    non-temporal stream reads — what bench.py's random_line_model prices the kernel's PMC line counts with."""
+    out = (C.c_double * 3)()
+    N.check(N.wl.infw_wl_line_rates(dev_ordinal, out), "line_rates")
+    return {"l2_hit_G_per_s": round(out[0], 1), "l2_miss_G_per_s": round(out[1], 1), "stream_GB_per_s": round(out[2], 1)}

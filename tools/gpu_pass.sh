@@ -1,0 +1,78 @@
+#!/bin/bash
+# One GPU pass, parameterised (replaces round 3's ~40 one-off tools/gpu_r03*.sh).  Runs on the GPU box via gpurun:
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_pass.sh <tag> <step> [<step> ...]
+# steps (in the order given; the pass stops at the first failing step, and no GPU step follows a fault or timeout):
+#   suite        pytest -m gpu (as the driver runs it, with per-test timeouts) and __graft_entry__.smoke()
+#   test:<expr>  pytest -m gpu -k <expr> (one test group)
+#   bench        the default bench line (what the driver's BENCH record runs)
+#   lines        every bench.py workload line (tools/bench_all.sh)
+#   line:<key>   one workload line: key as in prof:<key>
+#   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
+#                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3
+#   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
+#   ab:<script>  an A/B script under tools/ (tools/<script>.sh <tag>)
+# Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
+set -u
+TAG=${1:?tag}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+
+args_of() {  # bench.py arguments of a workload key
+  case $1 in
+    cfg2)   echo "" ;;
+    cfg2c)  echo "--layout compact" ;;
+    cfg1)   echo "--cfg 1 --batch 67108864" ;;
+    cfg4)   echo "--cfg 4" ;;
+    cfg4m)  echo "--cfg 4 --prefixes 1000000" ;;
+    cfg2u)  echo "--uniform" ;;
+    cfg2d)  echo "--templates 1000000" ;;
+    cfg2dw) echo "--templates 1000000 --key-order workload" ;;
+    fused)  echo "--from-frames 128 --fused" ;;
+    frames) echo "--from-frames 128" ;;
+    cfg3)   echo "--global-packets 1073741824 --steps 10 --warmup 2" ;;
+    *) echo "unknown workload key $1" >&2; return 1 ;;
+  esac
+}
+
+step() {
+  local s=$1 rc=0
+  case $s in
+    suite)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+          > $O/pytest_gpu.log 2>&1 || rc=$?
+      tail -3 $O/pytest_gpu.log
+      [ $rc -eq 0 ] || return $rc
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || rc=$?
+      tail -1 $O/smoke.log ;;
+    test:*)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" \
+          > $O/pytest_${s#test:}.log 2>&1 || rc=$?
+      tail -3 $O/pytest_${s#test:}.log ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > $O/bench_default.log 2>&1 || rc=$?
+      tail -1 $O/bench_default.log | cut -c1-400 ;;
+    lines)
+      bash tools/bench_all.sh $O/lines || rc=$? ;;
+    line:*)
+      local a; a=$(args_of ${s#line:}) || return 2
+      timeout -k 10 300 python -u bench.py $a --no-cpu-baseline > $O/line_${s#line:}.log 2>&1 || rc=$?
+      tail -1 $O/line_${s#line:}.log | cut -c1-300 ;;
+    prof:*)
+      local a; a=$(args_of ${s#prof:}) || return 2
+      [ "${s#prof:}" = cfg3 ] && a="--global-packets 1073741824"
+      bash tools/profile.sh ${TAG}_${s#prof:} $a --steps 5 --warmup 1 --no-cpu-baseline || rc=$? ;;
+    micro)
+      timeout -k 10 300 ./tools/micro/gather > $O/gather.jsonl 2>&1 || rc=$? ;;
+    ab:*)
+      timeout -k 10 1000 bash tools/${s#ab:}.sh $TAG > $O/${s#ab:}.log 2>&1 || rc=$?
+      tail -5 $O/${s#ab:}.log ;;
+    *) echo "unknown step $s"; return 2 ;;
+  esac
+  echo "step $s rc=$rc"
+  return $rc
+}
+
+for s in "$@"; do
+  step $s || { echo "pass $TAG stopped at $s"; exit 1; }
+done
+echo "pass $TAG all-ok"

@@ -93,10 +93,10 @@ def main():
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     # the traffic file bench.py reads for this workload: every figure from this one profile
     if line and "hbm_bytes_per_packet" in out:
-        rates = json.load(open(os.path.join(ROOT, "profiles", "line_rates.json")))
+        # (the line rates the bench's random_line_model prices these counts with are measured by bench.py itself,
+        # in its own process, before its timed loop — not stored here)
         tj = {"tag": tag, "workload_key": key, "build_id": line.get("build_id"), "kernel": line["roofline"]["kernel"],
-              "layout": layout,
-              "note": f"classify kernel, {key} bench command; see profiles/{tag}/summary.json", "line_rates": rates}
+              "layout": layout, "note": f"classify kernel, {key} bench command; see profiles/{tag}/summary.json"}
         for k in ("hbm_bytes_per_packet", "hbm_bytes_per_packet_raw", "l2_hits_per_packet", "l2_misses_per_packet",
                   "lds_bank_conflict_rate", "ea_rdreq_per_packet"):
             if k in out:
