@@ -474,7 +474,12 @@ struct infw_table_info {
                                /* short tables; chosen per full compile)       */
     uint32_t d16_permille;     /* of the /16s holding a prefix longer than /16, */
                                /* those a /16 word answers alone               */
-    uint64_t reserved[13];     /* zero; future fields come out of this         */
+    uint32_t split;            /* 1: the epoch classifies in two phases (LPM   */
+                               /* -> decision-line address per packet, then   */
+                               /* the decision lines as independent gathers):  */
+                               /* many distinct rule lists (INFW_SPLIT=0/1)    */
+    uint32_t pad1;
+    uint64_t reserved[12];     /* zero; future fields come out of this         */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
 #define INFW_COMMIT_INCREMENTAL 1u /* patched ranges copied into the spare image  */

@@ -162,9 +162,9 @@ struct KeyCount {
     }
     __device__ __forceinline__ uint32_t total() const { return (acc & 0xFFFFu) + (acc >> 16); }
 };
-__device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
-                                              uint32_t list, int cls, uint32_t v, uint32_t plog2, uint32_t p) {
-    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + infw_dt_slot_p(list, cls, v, plog2, p));
+__device__ __forceinline__ uint32_t dt_lookup_at(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
+                                                 uint64_t slot, uint32_t v) {
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + slot);
     u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
     if (a[0] & INFW_DT_ROOT) {
         KeyCount g(v);
@@ -202,6 +202,10 @@ __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ d
     r = k >= 8 ? d[2] : r;
     r = k >= 9 ? d[3] : r;
     return r;
+}
+__device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
+                                              uint32_t list, int cls, uint32_t v, uint32_t plog2, uint32_t p) {
+    return dt_lookup_at(dte, dtl, infw_dt_slot_p(list, cls, v, plog2, p), v);
 }
 
 // Longest /33../128 prefix covering an IPv6 address (infw_v6_long, device form):
@@ -310,6 +314,8 @@ struct BatchIn {
     const uint64_t *offsets;
     uint64_t fstride;
     const uint32_t *linear_len;
+    // kSplit (the two-phase form): phase 1 writes one word per packet here (split_word), phase 2 reads it
+    uint64_t *mid;
 };
 
 // ---- raw frames (kF): the tuple of infw_pack_header() (infw_pack.h) built in the kernel from the frame's
@@ -391,12 +397,100 @@ __device__ __noinline__ void dbg_insert(const DebugSink &d, const uint32_t k[6])
     }
 }
 
+// ---- the two-phase form (infw_dev_tables.split; chosen at commit for epochs with many distinct rule lists,
+// abi.cpp bind_view).  In the fused kernel every decision-line read depends on the packet's LPM answer; when the
+// entry lines span GiBs (one list per key, random update order) each such dependent read pays for the span (DESIGN.md
+// §7: dependent read pairs 27 -> 19 G/s from a 1- to a 12-GiB span, independent reads 53-57 G/s at any span).  Phase 1
+// (classify_kernel<..., kSplit>) walks the LPM and writes one word per packet; phase 2 (decide_kernel) reads those
+// words as a stream and the entry lines as independent gathers, then does the counters, results and verdicts.
+// Word: bit 63 = a decision line to read: entry-line index in bits 0..30, the packet value (dport or type << 8 |
+// code) in bits 31..46, min(frame length, 0xFFFF) in bits 47..62 (0xFFFF: read pkt_len); else 0 (no list: result 0)
+// or 1 (too short: XDP_DROP, kernel.c:423-426).
+__device__ __forceinline__ uint64_t split_word(uint64_t slot, uint32_t val, uint32_t plen) {
+    return 1ull << 63 | (uint64_t)(plen < 0xFFFFu ? plen : 0xFFFFu) << 47 | (uint64_t)val << 31 | slot;
+}
+
+template <int kBlock>
+__global__ __launch_bounds__(kBlock) void decide_kernel(const infw_dev_tables T, const uint64_t *__restrict__ mid,
+                                                        const uint32_t *__restrict__ pkt_len, uint64_t n,
+                                                        uint32_t *__restrict__ results, uint8_t *__restrict__ verdicts,
+                                                        unsigned long long *__restrict__ stats) {
+    __shared__ unsigned long long s_c[2 * kLdsStatKeys];  // as classify_kernel's: packets << 40 | bytes
+    for (int i = threadIdx.x; i < 2 * kLdsStatKeys; i += kBlock) s_c[i] = 0;
+    auto flush_counters = [&]() {
+        for (int s = threadIdx.x; s < 2 * kLdsStatKeys; s += kBlock) {
+            const unsigned long long c = s_c[s];
+            if (c) {
+                unsigned long long *dst = stats + (s >> 1) * 4 + (s & 1) * 2;
+                atomicAdd(dst, c >> 40);
+                atomicAdd(dst + 1, c & kBytesMask);
+                s_c[s] = 0;
+            }
+        }
+    };
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint32_t tiles_since_flush = 0;
+    uint64_t nw = 0;  // the next tile's word, loaded a tile ahead
+    {
+        const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (i0 < n) nw = __builtin_nontemporal_load(&mid[i0]);
+    }
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        const uint64_t w = valid ? nw : 0;
+        if (i + stride < n) nw = __builtin_nontemporal_load(&mid[i + stride]);
+        uint32_t result = 0, plen = 0;
+        if (w >> 63) {
+            plen = (uint32_t)(w >> 47) & 0xFFFFu;
+            if (plen == 0xFFFFu) plen = pkt_len[i];
+            result = dt_lookup_at(T.dte, T.dtl, w & 0x7FFFFFFFull, (uint32_t)(w >> 31) & 0xFFFFu);
+        }
+        // ---- verdict (kernel.c:444-456) and statistics (kernel.c:376-387), as in classify_kernel
+        const uint32_t action = result & 0xFFu;
+        const uint32_t key = (result >> 8) & 0xFFFFu;
+        const int s0_ = ((action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
+                            ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
+        const bool lds = plen < kBigLen && key < (uint32_t)kLdsStatKeys;
+        if (s0_ >= 0 && !lds) {
+            unsigned long long *dst = stats + (s0_ >> 1) * 4 + (s0_ & 1) * 2;
+            atomicAdd(dst, 1ull);
+            atomicAdd(dst + 1, (unsigned long long)plen);
+        }
+        const int s = lds ? s0_ : -1;
+        const uint64_t elig = __ballot(s >= 0);
+        if (elig) {
+            const int lead = __builtin_ctzll(elig);
+            const int s0 = __builtin_amdgcn_readlane(s, lead);
+            const bool mine = s == s0;
+            const uint64_t grp = __ballot(mine);
+            const uint32_t by = wave_sum(mine ? plen : 0u);
+            if (lane == lead) atomicAdd(&s_c[s0], (unsigned long long)__popcll(grp) << 40 | by);
+            if (s >= 0 && !mine) atomicAdd(&s_c[s], 1ull << 40 | plen);
+        }
+        if (valid) {
+            if (results) __builtin_nontemporal_store(result, &results[i]);
+            if (verdicts) verdicts[i] = (w == 1u || action == INFW_XDP_DROP) ? INFW_XDP_DROP : INFW_XDP_PASS;
+        }
+        if (++tiles_since_flush == T.stat_flush_tiles) {  // every workgroup runs the same number of tiles
+            __syncthreads();
+            flush_counters();
+            __syncthreads();
+            tiles_since_flush = 0;
+        }
+    }
+    __syncthreads();
+    flush_counters();
+}
+
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = four
 // 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
           bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false,
-          bool kD16 = false>
+          bool kD16 = false, bool kSplit = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -777,6 +871,19 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             else if (l1) d = T.desc[(uint64_t)(l1 - 1) * INFW_DESC_STRIDE + cls];
         }
         const uint32_t off = (uint32_t)d, cnt = (uint32_t)(d >> 32);
+        if (kSplit) {  // phase 1 of the two-phase form: the packet's decision-line address instead of the decision
+            if (valid) {
+                uint64_t w = pk == INFW_PK_DROP_SHORT ? 1u : 0u;
+                if (lst) {
+                    uint32_t p = T.dt_plog2;
+                    if (kPl) p = infw_dt_parts_of(s_pl[(lst - 1) & (INFW_DT_PL_LISTS - 1)], lst - 1, INFW_DT_PL_LISTS, cls, p);
+                    else if (T.n_dt_pl && lst - 1 < T.n_dt_pl) p = (T.dt_pl[lst - 1] >> (3 * cls)) & 7u;
+                    w = split_word(infw_dt_slot_p(lst - 1, cls, val, T.dt_plog2, p), val, plen);
+                }
+                __builtin_nontemporal_store(w, &in.mid[i]);
+            }
+            continue;  // no counters, results or verdicts in phase 1 (uniform over the workgroup: no barrier skipped)
+        }
 
         uint32_t result = 0;
         if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32) ^ lst;  // diagnostic 2: no first-match stage
@@ -893,14 +1000,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false>
+          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false, bool kSplit = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16, kSplit>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -942,6 +1049,59 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     return true;
 }
 
+// Phase 1 of the two-phase form: the default 768 x 2 shape of the epoch's kind, writing split words.
+template <bool kC, bool kLean, bool kPl, bool kD16>
+void launch_phase1(uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n, unsigned long long *st,
+                   hipStream_t stream) {
+    constexpr int kLog = kPl && kD16 ? 11 : 12;
+    launch<768, 0, 0, false, 6, false, kC, kLog, 9, kLean, false, 2, kPl, kD16, true>(2, cus, T, in, n, nullptr, nullptr,
+                                                                                       st, stream);
+}
+template <bool kC>
+void launch_phase1_of(uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n, unsigned long long *st,
+                      hipStream_t stream) {
+    const bool pl = T->n_dt_pl == INFW_DT_PL_LISTS, d16 = T->d16_on != 0;
+    if (T->lean) {
+        if (pl && d16) launch_phase1<kC, true, true, true>(cus, T, in, n, st, stream);
+        else if (pl) launch_phase1<kC, true, true, false>(cus, T, in, n, st, stream);
+        else if (d16) launch_phase1<kC, true, false, true>(cus, T, in, n, st, stream);
+        else launch_phase1<kC, true, false, false>(cus, T, in, n, st, stream);
+    } else {
+        if (pl && d16) launch_phase1<kC, false, true, true>(cus, T, in, n, st, stream);
+        else if (pl) launch_phase1<kC, false, true, false>(cus, T, in, n, st, stream);
+        else if (d16) launch_phase1<kC, false, false, true>(cus, T, in, n, st, stream);
+        else launch_phase1<kC, false, false, false>(cus, T, in, n, st, stream);
+    }
+}
+
+// The two-phase form (see decide_kernel): the split words live in stream-ordered scratch (hipMallocAsync from the
+// device's default pool, kept mapped between calls), so concurrent classify calls on other streams never share it.
+int launch_split(const infw_dev_tables *T, BatchIn bi, uint64_t n, uint32_t *results, uint8_t *verdicts,
+                 unsigned long long *st, uint32_t cus, hipStream_t stream, bool compact) {
+    static bool pool_kept[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -5;
+    if (dev < 64 && !pool_kept[dev]) {
+        hipMemPool_t pool;
+        uint64_t keep = ~0ull;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess)
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        pool_kept[dev] = true;
+    }
+    uint64_t *mid = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void **>(&mid), n * sizeof(uint64_t), stream) != hipSuccess) return -5;
+    bi.mid = mid;
+    if (compact) launch_phase1_of<true>(cus, T, &bi, n, st, stream);
+    else launch_phase1_of<false>(cus, T, &bi, n, st, stream);
+    constexpr int kB = 512;
+    const uint64_t tiles = (n + kB - 1) / kB, grid = 4ull * cus;
+    hipLaunchKernelGGL(decide_kernel<kB>, dim3((uint32_t)(tiles < grid ? tiles : grid)), dim3(kB), 0, stream, *T,
+                       (const uint64_t *)mid, bi.pkt_len, n, results, verdicts, st);
+    const bool ok = hipGetLastError() == hipSuccess;
+    (void)hipFreeAsync(mid, stream);
+    return ok ? 0 : -5;
+}
+
 }  // namespace
 
 // Host-side launcher (called from abi.cpp).
@@ -981,6 +1141,9 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
+    // the two-phase form for epochs that chose it (abi.cpp bind_view), in the default launch shape
+    if (T->split && group == 0 && block == 768 && bpc == 2 && !getenv("INFW_ABLATE") && !getenv("INFW_LDS_ABLATE"))
+        return launch_split(T, bi, n, results, verdicts, st, cus, stream, in_c != nullptr);
     // LDS attribution (diagnostic, tools/lds_ablate.sh): the default lean shape without one LDS structure each —
     // 1 the DIR-24-8 word cache, 2 the IPv6 group cache, 4 the LDS counters (no statistics: results stay valid,
     // counters do not), 7 all three.  SQ_LDS_BANK_CONFLICT of the default minus each variant attributes the rate.

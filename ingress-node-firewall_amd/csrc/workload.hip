@@ -378,13 +378,14 @@ int infw_wl_line_rates(int dev, double *out) {
     if (!out || hipSetDevice(dev) != hipSuccess) return -ENODEV;
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t grid = (uint32_t)(cus > 0 ? cus : 256) * 4;
+    const uint32_t grid = (uint32_t)(cus > 0 ? cus : 256) * 4;  // gathers: grid blocks, the stream: 2 * grid blocks
     const uint64_t big = 2ull << 30;
+    const size_t sink_words = (size_t)2 * grid * 512;            // one word per thread of the largest launch
     lr_u32x4 *tab = nullptr;
     uint32_t *sink = nullptr;
     hipEvent_t a = nullptr, b = nullptr;
     int rc = 0;
-    if (hipMalloc(&tab, big) != hipSuccess || hipMalloc(&sink, (size_t)grid * 512 * 4) != hipSuccess ||
+    if (hipMalloc(&tab, big) != hipSuccess || hipMalloc(&sink, sink_words * 4) != hipSuccess ||
         hipMemset(tab, 1, big) != hipSuccess || hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
         rc = -ENOMEM;
     auto timed = [&](auto launch, int reps) -> double {  // ms per launch after one untimed launch

@@ -122,7 +122,8 @@ class TableInfo(C.Structure):
                 ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("v6_slot_buckets", C.c_uint64),
                 ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32),
                 ("device_ms_max", C.c_double), ("n_device_slots", C.c_uint32), ("imported", C.c_uint32),
-                ("d16", C.c_uint32), ("d16_permille", C.c_uint32), ("reserved", C.c_uint64 * 13)]
+                ("d16", C.c_uint32), ("d16_permille", C.c_uint32), ("split", C.c_uint32),
+                ("pad1", C.c_uint32), ("reserved", C.c_uint64 * 12)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12

@@ -170,7 +170,7 @@ class Classifier:
     def info(self) -> Dict[str, float]:
         ti = N.TableInfo()
         check(N.lib.infw_table_info(self._ctx, C.byref(ti)), "info")
-        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f not in ("pad0", "reserved")}
+        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f not in ("pad0", "pad1", "reserved")}
         d["full_reason"] = ti.full_reason.decode()
         return d
 
