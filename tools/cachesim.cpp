@@ -123,6 +123,7 @@ int main(int argc, char **argv) {
     const uint32_t npfx = getenv("CACHESIM_PREFIXES") ? (uint32_t)atoi(getenv("CACHESIM_PREFIXES")) : 0;
     const uint32_t ntpl = getenv("CACHESIM_TEMPLATES") ? (uint32_t)atoi(getenv("CACHESIM_TEMPLATES")) : 0;
     if (infw_wl_create(&wl, cfg, 0x1F000000ull + cfg, npfx, ntpl)) return 1;
+    if (getenv("CACHESIM_UNIFORM") && atoi(getenv("CACHESIM_UNIFORM"))) infw_wl_uniform_sources(wl);  // bench --uniform
     PendingMap m;
     m.max_entries = 1u << 22;
     const uint64_t ne = infw_wl_n_entries(wl);
