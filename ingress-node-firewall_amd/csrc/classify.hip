@@ -1094,7 +1094,12 @@ int launch_split(const infw_dev_tables *T, BatchIn bi, uint64_t n, uint32_t *res
     if (compact) launch_phase1_of<true>(cus, T, &bi, n, st, stream);
     else launch_phase1_of<false>(cus, T, &bi, n, st, stream);
     constexpr int kB = 512;
-    const uint64_t tiles = (n + kB - 1) / kB, grid = 4ull * cus;
+    static const uint64_t bpc = [] {  // resident decide workgroups per CU (tuning: INFW_DECIDE_BPC)
+        const char *e = getenv("INFW_DECIDE_BPC");
+        const int v = e ? atoi(e) : 0;
+        return (uint64_t)(v >= 1 && v <= 4 ? v : 4);
+    }();
+    const uint64_t tiles = (n + kB - 1) / kB, grid = bpc * cus;
     hipLaunchKernelGGL(decide_kernel<kB>, dim3((uint32_t)(tiles < grid ? tiles : grid)), dim3(kB), 0, stream, *T,
                        (const uint64_t *)mid, bi.pkt_len, n, results, verdicts, st);
     const bool ok = hipGetLastError() == hipSuccess;
