@@ -529,7 +529,8 @@ def run_rank(args):
     digest = stats_digest(digest_block.cpu().numpy())
     block, group, bpc = clf.launch()
     kernel = f"classify_kernel<{block}, {group}> ({bpc} workgroups per CU)" + (
-        " (family-compact layout)" if args.layout == "compact" else "")
+        " (family-compact layout)" if args.layout == "compact" else "") + (
+        " + decide_kernel<512> (two-phase form)" if info.get("split") and not args.from_frames else "")
     if args.fused:
         kernel = "classify_kernel<768, 0> (2 workgroups per CU) (raw frames: infw_classify_frames)"
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,

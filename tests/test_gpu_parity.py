@@ -780,17 +780,20 @@ def test_debug_lookup_capture():
     assert np.array_equal(gres_b, m.classify_frames(hb, cb, pb, ib, nthreads=8)[0])
 
 
-@pytest.mark.parametrize("d16", ["", "1"])
-def test_incremental_commits_on_device(monkeypatch, d16):
+@pytest.mark.parametrize("d16,split", [("", ""), ("1", ""), ("", "1")])
+def test_incremental_commits_on_device(monkeypatch, d16, split):
     """§8f-2: a run of incremental commits (both device images ping-pong, one commit re-uploads
     after its new rule lists outgrow the spare's buffers); after every commit the device results
     equal the oracle's on the workload and on packets aimed at the edited prefixes — also with /16 words in
-    front of DIR-24-8 forced on, whose re-derived words the patch uploads with the rest."""
+    front of DIR-24-8 forced on, whose re-derived words the patch uploads with the rest, and in the two-phase
+    classify form (its decision lines patched and appended like the fused kernel's)."""
     import random
     import orc
     from test_incremental_cpu import _apply, _packets_for, _val
     if d16:
         monkeypatch.setenv("INFW_D16", d16)
+    if split:
+        monkeypatch.setenv("INFW_SPLIT", split)
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=100000, n_templates=512)
     ents = list(wl.entries())
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)

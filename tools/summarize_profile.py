@@ -56,19 +56,27 @@ def main():
     # packer path's classify_c that --fused checks its results against); PMC rows are filtered to it as well
     cls = [r for r in stats if "classify" in r["Name"]]
     main_name = max(cls, key=lambda r: int(r["Calls"]))["Name"] if cls else ""
+    # the two-phase form (classify.hip launch_split): phase 1 is a classify_kernel instantiation, phase 2 the
+    # decide_kernel launched as often — one classification is the pair, so times and counters are summed over both
+    calls = next((int(r["Calls"]) for r in stats if r["Name"] == main_name), 0)
+    names = [main_name] + [r["Name"] for r in stats if "decide_kernel" in r["Name"] and int(r["Calls"]) == calls]
+    names = list(dict.fromkeys(names))
+    out["split"] = len(names) > 1
     for r in stats:
-        if r["Name"] == main_name:
+        if r["Name"] in names:
             out["kernels"][r["Name"][:80]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                               "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
-    pmc = collections.defaultdict(list)
+    out["avg_ns_per_classification"] = sum(k["avg_ns"] for k in out["kernels"].values())
+    pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for name in sorted(os.listdir(src)):
         p = os.path.join(src, name, f"{name}_counter_collection.csv")
         if not name.startswith("pmc") or not os.path.exists(p):
             continue
         for r in csv.DictReader(open(p)):
-            if r["Kernel_Name"] == main_name:
-                pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    avg = {k: sum(v) / len(v) for k, v in pmc.items()}
+            if r["Kernel_Name"] in names:
+                pmc[r["Counter_Name"]][r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    # per classification: each kernel's average per launch, summed over the kernels of the pair
+    avg = {k: sum(sum(v) / len(v) for v in per.values()) for k, per in pmc.items()}
     out["pmc_avg_per_launch"] = avg
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
@@ -86,8 +94,7 @@ def main():
     if "TCC_EA0_RDREQ_sum" in avg:  # fabric read requests: one per 128-B line (MI355X_MICROARCH.md §HBM)
         out["ea_rdreq_per_packet"] = avg["TCC_EA0_RDREQ_sum"] / n
     if "GRBM_GUI_ACTIVE" in avg and out["kernels"]:
-        k = next(iter(out["kernels"].values()))
-        out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
+        out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / out["avg_ns_per_classification"]
     if line:
         out["bench_line_under_kernel_trace"] = line
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
