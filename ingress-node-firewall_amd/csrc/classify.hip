@@ -1076,6 +1076,7 @@ void launch_phase1_of(uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
 
 // The two-phase form (see decide_kernel): the split words live in stream-ordered scratch (hipMallocAsync from the
 // device's default pool, kept mapped between calls), so concurrent classify calls on other streams never share it.
+// Returns 0, -5 on a launch error, or 1 when the scratch cannot be allocated (the caller then runs the fused kernel).
 int launch_split(const infw_dev_tables *T, BatchIn bi, uint64_t n, uint32_t *results, uint8_t *verdicts,
                  unsigned long long *st, uint32_t cus, hipStream_t stream, bool compact) {
     static bool pool_kept[64] = {};
@@ -1089,7 +1090,10 @@ int launch_split(const infw_dev_tables *T, BatchIn bi, uint64_t n, uint32_t *res
         pool_kept[dev] = true;
     }
     uint64_t *mid = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void **>(&mid), n * sizeof(uint64_t), stream) != hipSuccess) return -5;
+    if (hipMallocAsync(reinterpret_cast<void **>(&mid), n * sizeof(uint64_t), stream) != hipSuccess) {
+        (void)hipGetLastError();  // no room for the words: the caller runs the fused kernel instead
+        return 1;
+    }
     bi.mid = mid;
     if (compact) launch_phase1_of<true>(cus, T, &bi, n, st, stream);
     else launch_phase1_of<false>(cus, T, &bi, n, st, stream);
@@ -1147,8 +1151,10 @@ extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_s
     }
     auto *st = reinterpret_cast<unsigned long long *>(stats);
     // the two-phase form for epochs that chose it (abi.cpp bind_view), in the default launch shape
-    if (T->split && group == 0 && block == 768 && bpc == 2 && !getenv("INFW_ABLATE") && !getenv("INFW_LDS_ABLATE"))
-        return launch_split(T, bi, n, results, verdicts, st, cus, stream, in_c != nullptr);
+    if (T->split && group == 0 && block == 768 && bpc == 2 && !getenv("INFW_ABLATE") && !getenv("INFW_LDS_ABLATE")) {
+        const int rc = launch_split(T, bi, n, results, verdicts, st, cus, stream, in_c != nullptr);
+        if (rc <= 0) return rc;  // 1: scratch allocation failed, fall through to the fused kernel
+    }
     // LDS attribution (diagnostic, tools/lds_ablate.sh): the default lean shape without one LDS structure each —
     // 1 the DIR-24-8 word cache, 2 the IPv6 group cache, 4 the LDS counters (no statistics: results stay valid,
     // counters do not), 7 all three.  SQ_LDS_BANK_CONFLICT of the default minus each variant attributes the rate.
