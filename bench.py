@@ -550,7 +550,8 @@ def run_rank(args):
     else:
         extra_pipe = {}
     wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_uniform" if args.uniform else "") + (
-        "_frames" if args.from_frames else "") + ("_fused" if args.fused else "")
+        "_frames" if args.from_frames else "") + ("_fused" if args.fused else "") + (
+        "_compact" if args.layout == "compact" and not args.from_frames else "")
 
     traffic = None
     traffic_from = None
@@ -593,6 +594,9 @@ def run_rank(args):
             if "ea_rdreq_per_packet" in tj:
                 extra["line_traffic_GBps_at_128B"] = round(tj["ea_rdreq_per_packet"] * 128 * n / (avg_kern_ms * 1e-3)
                                                            / 1e9, 1)
+                if rates:  # the fabric's line traffic against the stream bandwidth this process measured
+                    extra["line_traffic_frac_of_stream"] = round(extra["line_traffic_GBps_at_128B"] /
+                                                                 rates["stream_GB_per_s"], 3)
                 extra["fetch_size_GBps"] = round(traffic / (avg_kern_ms * 1e-3) / 1e9, 1) if traffic else None
             if "lds_bank_conflict_rate" in tj:
                 extra["lds_bank_conflict_rate"] = round(tj["lds_bank_conflict_rate"], 4)

@@ -37,6 +37,8 @@ def main():
     if os.environ.get("PROFILE_KEY"):  # a line profiled before bench.py named its table size in the key
         key = os.environ["PROFILE_KEY"]
     layout = line.get("roofline", {}).get("layout", "standard")
+    if layout == "compact" and not key.endswith("_compact") and "_frames" not in key:  # lines before round 4's key
+        key += "_compact"
     if line:
         n = line["config"]["packets_per_gpu_per_step"]
     stream_b = 32.0  # tuple bytes read per packet
