@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/infw.h"
 #include "infw_tables.h"
@@ -1012,6 +1013,14 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
 
+bool d16_big() {
+    static const bool big = [] {
+        const char *e = getenv("INFW_D16_CACHE");
+        return e && strcmp(e, "big") == 0;
+    }();
+    return big;
+}
+
 // The decision-table kernel without sidebands: launch shape (block, resident blocks per CU) and
 // LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.  Blocks are
 // multiples of 256 threads: other sizes spread their waves unevenly over the 4 SIMDs (measured
@@ -1028,10 +1037,15 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form; with
     // per-list part counts their LDS copy takes half the word cache (INFW_DT_ADAPT=0 at compile: none)
     // sparse short tables with /16 words (d16_on), with and without per-list part counts
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on && T->n_dt_pl == INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    // (INFW_D16_CACHE=big, A/B: the /16-word cache doubled into LDS the shape leaves free — 2048 entries beside the
+    // part counts, 4096 without them and a 256-entry IPv6 group cache; 68 / 76 KiB per workgroup)
+    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on && T->n_dt_pl == INFW_DT_PL_LISTS) {
+        if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    } else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on) {
+        if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+    }
     // with per-list part counts (16 KiB of LDS) a 4096-entry word cache and a 256-entry IPv6 group cache: same-box
     // alternating A/B against 2048 + 512 at configs[2], 2.361 vs 2.378 ms (profiles/r03zc)
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
