@@ -1016,7 +1016,7 @@ void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const 
 bool d16_big() {
     static const bool big = [] {
         const char *e = getenv("INFW_D16_CACHE");
-        return e && strcmp(e, "big") == 0;
+        return !(e && strcmp(e, "small") == 0);
     }();
     return big;
 }
@@ -1037,8 +1037,9 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
     // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form; with
     // per-list part counts their LDS copy takes half the word cache (INFW_DT_ADAPT=0 at compile: none)
     // sparse short tables with /16 words (d16_on), with and without per-list part counts
-    // (INFW_D16_CACHE=big, A/B: the /16-word cache doubled into LDS the shape leaves free — 2048 entries beside the
-    // part counts, 4096 without them and a 256-entry IPv6 group cache; 68 / 76 KiB per workgroup)
+    // the /16-word cache takes the LDS the shape leaves free — 2048 entries beside the part counts, 4096 without them
+    // and a 256-entry IPv6 group cache (68 / 76 KiB per workgroup): same-box alternating A/B against half of it
+    // (INFW_D16_CACHE=small), configs[1] 1.154 -> 1.108 ms (+4 %), configs[4] even (profiles/r04g)
     else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on && T->n_dt_pl == INFW_DT_PL_LISTS) {
         if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
         else launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);

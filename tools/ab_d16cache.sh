@@ -1,5 +1,5 @@
 #!/bin/bash
-# The /16-word LDS cache at its default size against the doubled one (INFW_D16_CACHE=big) on the workloads with /16
+# The /16-word LDS cache halved (INFW_D16_CACHE=small) against the default on the workloads with /16
 # words — configs[1] and configs[4] — alternated twice on one box.  Usage: tools/ab_d16cache.sh <tag>
 set -u
 O=gpurun_out/${1:-ab}/ab_d16cache
@@ -14,9 +14,9 @@ run() {
   [ $rc -eq 0 ] || exit $rc
 }
 for rep in 1 2; do
-  run cfg1_default_r$rep INFW_D16_CACHE=default -- --cfg 1 --batch 67108864
+  run cfg1_default_r$rep INFW_D16_CACHE=small -- --cfg 1 --batch 67108864
   run cfg1_big_r$rep INFW_D16_CACHE=big -- --cfg 1 --batch 67108864
-  run cfg4_default_r$rep INFW_D16_CACHE=default -- --cfg 4
+  run cfg4_default_r$rep INFW_D16_CACHE=small -- --cfg 4
   run cfg4_big_r$rep INFW_D16_CACHE=big -- --cfg 4
 done
 echo ab-d16cache-ok
