@@ -1074,9 +1074,13 @@ def test_lds_d16_cache_collisions(monkeypatch):
     assert len(np.unique(want[want != 0])) > 60
 
 
-def test_classify_host_batches():
+@pytest.mark.parametrize("split", ["", "1"])
+def test_classify_host_batches(monkeypatch, split):
     """infw_classify_host: a host-resident batch pipelined through the device in chunks (ragged last chunk,
-    pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle."""
+    pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle — also in
+    the two-phase form, whose per-chunk scratch is allocated on the pipeline's kernel stream."""
+    if split:
+        monkeypatch.setenv("INFW_SPLIT", split)
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
