@@ -86,6 +86,8 @@ struct Variant {
                       // of its home set; the lookup reads the home set's line)
     int d16 = 0;      // 1: an 8-B word per (slot, /16) in front of DIR-24-8 answers /16s of <= 3 runs (A | B | A, values
                       // <= 15 bits) by itself; other /16s read their tbl24 word after it
+    int mphf = 0;     // > 0: IPv6 groups in a dense array of mphf-byte records at their rank under a minimal perfect
+                      // hash (a random permutation of the groups); an absent group reads one record at a hashed rank
 };
 
 // Does (slot, /16 hi) have at most three runs of the A | B | A shape with values <= 0x7FFF?
@@ -178,6 +180,8 @@ int main(int argc, char **argv) {
                             {"set4", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 0},
                             {"set4_d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 1},
                             {"lp2_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.8},
+                            {"mphf32", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 0, 0, 32},
+                            {"mphf64", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 0, 0, 64},
                             {"lp2_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.6},
                             {"lp4_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.8},
                             {"lp4_60", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 4, 0.6},
@@ -497,6 +501,25 @@ int main(int argc, char **argv) {
                     if (V.set4) {  // slots needed: one per record of every group (n_buckets groups, ~1.3 records each)
                         const uint64_t sets = std::max<uint64_t>(1, (uint64_t)(h.n_buckets * 1.31 / (4 * 0.8)));
                         tc[nt - 1].addr = 7 * kSpace + (infw_bucket_hash((uint32_t)slot, a32) % sets) * 128;
+                    }
+                    if (V.mphf) {
+                        static std::unordered_map<uint64_t, uint64_t> rank;
+                        if (rank.empty()) {
+                            std::vector<uint64_t> gk;
+                            for (const infw_v6_bucket &b : h.btab)
+                                if (b.tag) gk.push_back((uint64_t)(b.tag - 1) << 32 | b.top);
+                            std::sort(gk.begin(), gk.end());
+                            uint64_t r = 0x9E3779B97F4A7C15ull;
+                            for (size_t j = gk.size(); j > 1; j--) {  // Fisher-Yates with a fixed seed
+                                r = r * 6364136223846793005ull + 1442695040888963407ull;
+                                std::swap(gk[j - 1], gk[(r >> 33) % j]);
+                            }
+                            for (size_t j = 0; j < gk.size(); j++) rank[gk[j]] = j;
+                        }
+                        const uint64_t gkey = (uint64_t)slot << 32 | a32;
+                        auto it = rank.find(gkey);
+                        const uint64_t rk = it != rank.end() ? it->second : infw_bucket_hash((uint32_t)slot, a32) % rank.size();
+                        tc[nt - 1].addr = 10 * kSpace + rk * V.mphf;
                     }
                     if (V.cuckoo) {
                         const uint64_t gk = (uint64_t)slot << 32 | a32;
