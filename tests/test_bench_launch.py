@@ -49,6 +49,10 @@ def test_gpus_2_spawns_two_ranks_same_digest():
     four = _line(_bench("--gpus", "4", *common))  # the driver's scaling run uses 1, 2, 4, 8 ranks
     assert four["rccl_world_size"] == 4 and four["config"]["stats_digest"] == one["config"]["stats_digest"]
     assert [r["tables"] for r in four["per_rank"]] == ["compiled"] + ["imported"] * 3
+    eight = _line(_bench("--gpus", "8", *common))  # the 8-GPU node's rank count (image verified on 7 imports)
+    assert eight["rccl_world_size"] == 8 and eight["config"]["stats_digest"] == one["config"]["stats_digest"]
+    assert [r["tables"] for r in eight["per_rank"]] == ["compiled"] + ["imported"] * 7
+    assert sum(r["packets_per_step"] for r in eight["per_rank"]) == JOB
     # the digest is the whole job's counters, walked here in one piece
     import infw
     from bench import host_counters, stats_digest
