@@ -10,7 +10,7 @@
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
-#   ab:<script>  an A/B script under tools/ (tools/<script>.sh <tag>)
+#   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: split split2 split3 split4 d16cache cfg1_shape)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
 set -u
 TAG=${1:?tag}; shift
@@ -64,8 +64,8 @@ step() {
     micro)
       timeout -k 10 300 ./tools/micro/gather > $O/gather.jsonl 2>&1 || rc=$? ;;
     ab:*)
-      timeout -k 10 1000 bash tools/${s#ab:}.sh $TAG > $O/${s#ab:}.log 2>&1 || rc=$?
-      tail -5 $O/${s#ab:}.log ;;
+      timeout -k 10 1000 bash tools/ab.sh $TAG ${s#ab:} > $O/ab_${s#ab:}.log 2>&1 || rc=$?
+      tail -5 $O/ab_${s#ab:}.log ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
   echo "step $s rc=$rc"
