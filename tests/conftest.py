@@ -13,5 +13,16 @@ for p in (ROOT, os.path.join(ROOT, "ingress-node-firewall_amd"), os.path.join(RO
         sys.path.insert(0, p)
 
 
+def run_make(*targets, timeout=900):
+    """`make -s -C ROOT targets` under an exclusive lock on build/.make.lock: tests in parallel workers (pytest -n)
+    that build the same sanitizer targets must not write the same objects at once."""
+    import fcntl
+    import subprocess
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return subprocess.run(["make", "-s", "-C", ROOT, *targets], capture_output=True, text=True, timeout=timeout)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); runs the HIP classifier")

@@ -294,7 +294,8 @@ def test_host_sanitizer_walk():
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run(["make", "-s", "asan"], cwd=root, capture_output=True, text=True, timeout=600)
+    from conftest import run_make
+    r = run_make("asan", timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
     # the same harness with the IPv6 groups in the two-choice slot form (cuckoo placement, in-place patching)
     env = dict(os.environ, INFW_V6_FORM="b2", ASAN_CHURN_ROUNDS="3")

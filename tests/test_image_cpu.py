@@ -338,8 +338,8 @@ def test_host_sanitizer_abi_and_images(tmp_path):
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
     root = os.path.dirname(ASAN_ABI)
-    r = subprocess.run(["make", "-s", "asan-host"], cwd=os.path.dirname(os.path.dirname(os.path.dirname(root))),
-                       capture_output=True, text=True, timeout=900)
+    from conftest import run_make
+    r = run_make("asan-host")
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     r = subprocess.run([ASAN_ABI], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-3000:]

@@ -10,6 +10,7 @@ import pytest
 
 import goenc
 import infw
+from conftest import run_make
 from test_golden import load
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,8 +24,7 @@ DRIVERS = pytest.mark.parametrize("drv", [DRIVER, ASAN_DRIVER], ids=["lib", "asa
 @pytest.fixture(scope="module", autouse=True)
 def driver():
     if not os.path.exists(DRIVER):  # built by `make` (the GPU box gets it with the libraries)
-        r = subprocess.run(["make", "-s", "-C", ROOT, os.path.relpath(DRIVER, ROOT)], capture_output=True, text=True,
-                           timeout=600)
+        r = run_make(os.path.relpath(DRIVER, ROOT), timeout=600)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert os.path.exists(DRIVER)
 
@@ -34,7 +34,7 @@ def asan_driver():
     import shutil
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
-    r = subprocess.run(["make", "-s", "-C", ROOT, "asan-host"], capture_output=True, text=True, timeout=900)
+    r = run_make("asan-host")
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return ASAN_DRIVER
 
