@@ -176,9 +176,9 @@ int main(int argc, char **argv) {
                             {"mini4", false, false, 0, 64, 64, 0, 0, 4}, {"mini3", false, false, 0, 64, 64, 0, 0, 3},
                             {"adaptP", false, false, 0, 64, 64, 0, 0, 0, 0, 1},
                             {"clsP", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 1},
-                            {"d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 1},
-                            {"set4", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 0},
-                            {"set4_d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 1, 1},
+                            {"d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 0, 1},
+                            {"set4", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 1, 0},
+                            {"set4_d16", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 1, 1},
                             {"lp2_80", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 2, 0.8},
                             {"mphf32", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 0, 0, 32},
                             {"mphf64", false, false, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0.8, 0, 0, 64},
