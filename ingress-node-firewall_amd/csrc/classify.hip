@@ -165,30 +165,34 @@ struct KeyCount {
 };
 __device__ __forceinline__ uint32_t dt_lookup_at(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
                                                  uint64_t slot, uint32_t v) {
-    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + slot);
-    u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
+    // the line's first 32 B; the second 32 B only where they are needed (a root's keys, a u32-form leaf, a compact
+    // leaf of > 9 segments whose value lies past its key 8) — half-first compact layout, infw_tables.h
+    const u32x4 *L = reinterpret_cast<const u32x4 *>(dte + slot);
+    u32x4 a = L[0], b = L[1];
     if (a[0] & INFW_DT_ROOT) {
+        const u32x4 c = L[2], d = L[3];
         KeyCount g(v);
         g.add(a[1]); g.add(a[2]); g.add(a[3]); g.add(b[0]); g.add(b[1]); g.add(b[2]); g.add(b[3]);
         g.add(c[0]); g.add(c[1]); g.add(c[2]); g.add(c[3]); g.add(d[0]); g.add(d[1]); g.add(d[2]); g.add(d[3]);
-        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g.total()));
-        a = l[0];
-        b = l[1];
-        c = l[2];
-        d = l[3];
+        L = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g.total()));
+        a = L[0];
+        b = L[1];
     }
-    if (a[0] & INFW_DT_COMPACT) {  // 19 u16 keys in w[1..10], u8 result codes in w[11..15]
+    if (a[0] & INFW_DT_COMPACT) {
         KeyCount kc(v);
-        kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]); kc.add(b[2]); kc.add(b[3]);
-        kc.add(c[0]); kc.add(c[1]); kc.add(c[2]);
-        const uint32_t k = kc.total();
-        uint32_t w = c[3];
-        w = k >= 4 ? d[0] : w;
-        w = k >= 8 ? d[1] : w;
-        w = k >= 12 ? d[2] : w;
-        w = k >= 16 ? d[3] : w;
+        kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]);  // keys 0..7
+        uint32_t k = kc.total();
+        if (k == 8 && (a[0] & 0xFFu) > 9) {
+            const u32x4 c = L[2], d = L[3];
+            KeyCount k2(v);
+            k2.add(c[0]); k2.add(c[1]); k2.add(c[2]); k2.add(c[3]); k2.add(d[0]); k2.add(d[1]);  // keys 8..19
+            k += k2.total();
+            if (k >= 12) return infw_dt_code_result(__builtin_amdgcn_ubfe(k >= 16 ? d[3] : d[2], 8 * (k & 3u), 8));
+        }
+        const uint32_t w = k < 4 ? b[1] : k < 8 ? b[2] : b[3];  // codes 0..11
         return infw_dt_code_result(__builtin_amdgcn_ubfe(w, 8 * (k & 3u), 8));
     }
+    const u32x4 c = L[2], d = L[3];
     KeyCount kc(v);
     kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]);
     const uint32_t k = kc.total();

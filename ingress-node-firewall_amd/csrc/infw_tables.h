@@ -115,10 +115,13 @@ struct infw_v6_slot {       // 32 B
 //   compact leaf (w[0] bit 30; S <= 20): used when every result of the step
 //                function is 0 or SET_ACTIONRULE_RESPONSE(1|2, ruleId 1..127) —
 //                everything makeIngressFwRulesMap writes (loader.go:429-515):
-//                u16 keys in w[1..10], one result code per segment in the bytes
-//                of w[11..15]; code 0 = no match, else ruleId = code >> 1 and
-//                action = 1 + (code & 1).  Twice the segments of a u32 leaf, so
-//                half the leaf lines (and half the L2 footprint);
+//                n = w[0] & 0xFF segments, u16 keys and one result code per
+//                segment (bytes), half-first (infw_dt_ckey_word / _ccode_word):
+//                keys 0..7 and codes 0..11 in the first 32 B, the rest in the
+//                second, so the kernel reads the second half only for a value
+//                past key 8 of a leaf of > 9 segments; code 0 = no match, else
+//                ruleId = code >> 1 and action = 1 + (code & 1).  Twice the
+//                segments of a u32 leaf, so half the leaf lines;
 //   root form    (bit 31 set): 30 u16 group keys in w[1..15] select one of
 //                <= 31 leaf lines dtl[(w[0] & 0x3FFFFFFF) + #keys below v], each
 //                a leaf over 10 (u32) or 20 (compact) consecutive segments.
@@ -316,11 +319,19 @@ INFW_TD uint32_t infw_dt_result_code(uint32_t r) {
     return (a == 1u || a == 2u) && id >= 1u && id <= 127u ? (id << 1 | (a - 1u)) : 0x100u;
 }
 
+// Compact leaf (<= 20 segments, u8 result codes), half-first: w[0] = COMPACT | n; keys 0..7 in w[1..4], codes
+// 0..11 in w[5..7] — the first 32 B, which answer every value below key 8 and, when n <= 9, every value; keys 8..19
+// in w[8..13], codes 12..19 in w[14..15].  Key j (u16 half j & 1 of its word) = start of segment j + 1, minus 1
+// (0xFFFF past the last segment).
+INFW_TD uint32_t infw_dt_ckey_word(uint32_t j) { return j < 8 ? 1 + (j >> 1) : 8 + ((j - 8) >> 1); }
+INFW_TD uint32_t infw_dt_ccode_word(uint32_t j) { return j < 12 ? 5 + (j >> 2) : 14 + ((j - 12) >> 2); }
+
 // Result of a leaf line (u32 or compact form) for v.
 INFW_TD uint32_t infw_dt_leaf(const uint32_t *w, uint32_t v) {
     if (w[0] & INFW_DT_COMPACT) {
-        const uint32_t c = infw_keys_below(w, 1, 11, v);  // 0..19
-        return infw_dt_code_result((w[11 + (c >> 2)] >> (8 * (c & 3u))) & 0xFFu);
+        uint32_t c = infw_keys_below(w, 1, 5, v);  // 0..8
+        if (c == 8 && (w[0] & 0xFFu) > 9) c += infw_keys_below(w, 8, 14, v);  // 8..19
+        return infw_dt_code_result((w[infw_dt_ccode_word(c)] >> (8 * (c & 3u))) & 0xFFu);
     }
     const uint32_t c = infw_keys_below(w, 1, 6, v);
     uint32_t r = w[6];

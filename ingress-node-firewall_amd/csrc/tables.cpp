@@ -482,19 +482,17 @@ int PendingMap::next_key(const lpm_ip_key_st *key, lpm_ip_key_st *next) const {
 static void fill_leaf(infw_dt_line &l, const uint32_t *starts, const uint32_t *res, uint32_t n, bool compact) {
     memset(&l, 0, sizeof(l));
     const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS, kw = segs / 2;  // key words
-    for (uint32_t k = 0; k < kw; k++) {
-        uint32_t w = 0;
-        for (uint32_t h = 0; h < 2; h++) {
-            const uint32_t j = 2 * k + h;
-            w |= (uint32_t)(j + 1 < n ? (uint16_t)(starts[j + 1] - 1) : (uint16_t)0xFFFF) << (16 * h);
-        }
-        l.w[1 + k] = w;
-    }
-    if (compact) {
+    auto key = [&](uint32_t j) -> uint32_t { return j + 1 < n ? (uint16_t)(starts[j + 1] - 1) : 0xFFFFu; };
+    if (compact) {  // half-first: the first 32 B answer every value below key 8, and every value when n <= 9
         l.w[0] = INFW_DT_COMPACT | n;
-        for (uint32_t j = 0; j < segs; j++)
-            l.w[1 + kw + (j >> 2)] |= infw_dt_result_code(j < n ? res[j] : res[n - 1]) << (8 * (j & 3u));
-    } else {
+        for (uint32_t j = 0; j < INFW_DT_CLEAF_SEGS; j++) {
+            l.w[infw_dt_ckey_word(j)] |= key(j) << (16 * (j & 1u));
+            l.w[infw_dt_ccode_word(j)] |= infw_dt_result_code(j < n ? res[j] : res[n - 1]) << (8 * (j & 3u));
+        }
+        return;
+    }
+    for (uint32_t k = 0; k < kw; k++) l.w[1 + k] = key(2 * k) | key(2 * k + 1) << 16;
+    {
         l.w[0] = n;
         for (uint32_t j = 0; j < segs; j++) l.w[1 + kw + j] = j < n ? res[j] : res[n - 1];
     }
