@@ -478,7 +478,8 @@ struct infw_table_info {
                                /* -> decision-line address per packet, then   */
                                /* the decision lines as independent gathers):  */
                                /* many distinct rule lists (INFW_SPLIT=0/1)    */
-    uint32_t pad1;
+    uint32_t dt_half_reads;    /* 1: decision lines read half-first (nearly all */
+                               /* compact leaves of <= 9 segments; INFW_DT_HALF) */
     uint64_t reserved[12];     /* zero; future fields come out of this         */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */

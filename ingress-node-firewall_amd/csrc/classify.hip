@@ -163,18 +163,63 @@ struct KeyCount {
     }
     __device__ __forceinline__ uint32_t total() const { return (acc & 0xFFFFu) + (acc >> 16); }
 };
-__device__ __forceinline__ uint32_t dt_lookup_at(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
-                                                 uint64_t slot, uint32_t v) {
-    // the line's first 32 B; the second 32 B only where they are needed (a root's keys, a u32-form leaf, a compact
-    // leaf of > 9 segments whose value lies past its key 8) — half-first compact layout, infw_tables.h
+__device__ __forceinline__ uint32_t dt_u32_leaf(u32x4 a, u32x4 b, u32x4 c, u32x4 d, uint32_t v) {
+    KeyCount kc(v);
+    kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]);
+    const uint32_t k = kc.total();
+    uint32_t r = b[2];
+    r = k >= 1 ? b[3] : r;
+    r = k >= 2 ? c[0] : r;
+    r = k >= 3 ? c[1] : r;
+    r = k >= 4 ? c[2] : r;
+    r = k >= 5 ? c[3] : r;
+    r = k >= 6 ? d[0] : r;
+    r = k >= 7 ? d[1] : r;
+    r = k >= 8 ? d[2] : r;
+    r = k >= 9 ? d[3] : r;
+    return r;
+}
+__device__ __forceinline__ uint32_t dt_root_index(u32x4 a, u32x4 b, u32x4 c, u32x4 d, uint32_t v) {
+    KeyCount g(v);
+    g.add(a[1]); g.add(a[2]); g.add(a[3]); g.add(b[0]); g.add(b[1]); g.add(b[2]); g.add(b[3]);
+    g.add(c[0]); g.add(c[1]); g.add(c[2]); g.add(c[3]); g.add(d[0]); g.add(d[1]); g.add(d[2]); g.add(d[3]);
+    return (a[0] & INFW_DT_INDEX) + g.total();
+}
+// The whole 64-B line at once (four 16-B loads issued back to back); the compact leaf decoded without branches.
+__device__ __forceinline__ uint32_t dt_lookup_full(const infw_dt_line *__restrict__ dte,
+                                                   const infw_dt_line *__restrict__ dtl, uint64_t slot, uint32_t v) {
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(dte + slot);
+    u32x4 a = e[0], b = e[1], c = e[2], d = e[3];
+    if (a[0] & INFW_DT_ROOT) {
+        const u32x4 *l = reinterpret_cast<const u32x4 *>(dtl + dt_root_index(a, b, c, d, v));
+        a = l[0];
+        b = l[1];
+        c = l[2];
+        d = l[3];
+    }
+    if (a[0] & INFW_DT_COMPACT) {  // half-first layout (infw_tables.h): keys 0..7, codes 0..11, keys 8..19, codes 12..19
+        KeyCount kc(v);
+        kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]);
+        kc.add(c[0]); kc.add(c[1]); kc.add(c[2]); kc.add(c[3]); kc.add(d[0]); kc.add(d[1]);
+        const uint32_t k = kc.total();
+        uint32_t w = b[1];
+        w = k >= 4 ? b[2] : w;
+        w = k >= 8 ? b[3] : w;
+        w = k >= 12 ? d[2] : w;
+        w = k >= 16 ? d[3] : w;
+        return infw_dt_code_result(__builtin_amdgcn_ubfe(w, 8 * (k & 3u), 8));
+    }
+    return dt_u32_leaf(a, b, c, d, v);
+}
+// Half-first: the line's first 32 B; the second 32 B only where needed — a root's keys, a u32-form leaf, a compact
+// leaf of > 9 segments whose value lies past its key 8.  For epochs of short step functions (choose_dt_half).
+__device__ __forceinline__ uint32_t dt_lookup_half(const infw_dt_line *__restrict__ dte,
+                                                   const infw_dt_line *__restrict__ dtl, uint64_t slot, uint32_t v) {
     const u32x4 *L = reinterpret_cast<const u32x4 *>(dte + slot);
     u32x4 a = L[0], b = L[1];
     if (a[0] & INFW_DT_ROOT) {
         const u32x4 c = L[2], d = L[3];
-        KeyCount g(v);
-        g.add(a[1]); g.add(a[2]); g.add(a[3]); g.add(b[0]); g.add(b[1]); g.add(b[2]); g.add(b[3]);
-        g.add(c[0]); g.add(c[1]); g.add(c[2]); g.add(c[3]); g.add(d[0]); g.add(d[1]); g.add(d[2]); g.add(d[3]);
-        L = reinterpret_cast<const u32x4 *>(dtl + ((a[0] & INFW_DT_INDEX) + g.total()));
+        L = reinterpret_cast<const u32x4 *>(dtl + dt_root_index(a, b, c, d, v));
         a = L[0];
         b = L[1];
     }
@@ -192,25 +237,17 @@ __device__ __forceinline__ uint32_t dt_lookup_at(const infw_dt_line *__restrict_
         const uint32_t w = k < 4 ? b[1] : k < 8 ? b[2] : b[3];  // codes 0..11
         return infw_dt_code_result(__builtin_amdgcn_ubfe(w, 8 * (k & 3u), 8));
     }
-    const u32x4 c = L[2], d = L[3];
-    KeyCount kc(v);
-    kc.add(a[1]); kc.add(a[2]); kc.add(a[3]); kc.add(b[0]); kc.add(b[1]);
-    const uint32_t k = kc.total();
-    uint32_t r = b[2];
-    r = k >= 1 ? b[3] : r;
-    r = k >= 2 ? c[0] : r;
-    r = k >= 3 ? c[1] : r;
-    r = k >= 4 ? c[2] : r;
-    r = k >= 5 ? c[3] : r;
-    r = k >= 6 ? d[0] : r;
-    r = k >= 7 ? d[1] : r;
-    r = k >= 8 ? d[2] : r;
-    r = k >= 9 ? d[3] : r;
-    return r;
+    return dt_u32_leaf(a, b, L[2], L[3], v);
 }
+template <bool kHalf = false>
+__device__ __forceinline__ uint32_t dt_lookup_at(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
+                                                 uint64_t slot, uint32_t v) {
+    return kHalf ? dt_lookup_half(dte, dtl, slot, v) : dt_lookup_full(dte, dtl, slot, v);
+}
+template <bool kHalf = false>
 __device__ __forceinline__ uint32_t dt_lookup(const infw_dt_line *__restrict__ dte, const infw_dt_line *__restrict__ dtl,
                                               uint32_t list, int cls, uint32_t v, uint32_t plog2, uint32_t p) {
-    return dt_lookup_at(dte, dtl, infw_dt_slot_p(list, cls, v, plog2, p), v);
+    return dt_lookup_at<kHalf>(dte, dtl, infw_dt_slot_p(list, cls, v, plog2, p), v);
 }
 
 // Longest /33../128 prefix covering an IPv6 address (infw_v6_long, device form):
@@ -495,7 +532,7 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(const infw_dev_tables T,
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
           bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false,
-          bool kD16 = false, bool kSplit = false>
+          bool kD16 = false, bool kSplit = false, bool kHalf = false>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
@@ -897,7 +934,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             uint32_t p = T.dt_plog2;
             if (kPl) p = infw_dt_parts_of(s_pl[(lst - 1) & (INFW_DT_PL_LISTS - 1)], lst - 1, INFW_DT_PL_LISTS, cls, p);
             else if (T.n_dt_pl && lst - 1 < T.n_dt_pl) p = (T.dt_pl[lst - 1] >> (3 * cls)) & 7u;
-            result = dt_lookup(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2, p);
+            result = dt_lookup<kHalf>(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2, p);
         }
         // ---- first match, one lane per rule, G packets in flight
         uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
@@ -1005,14 +1042,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
 
 template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
           bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false, bool kSplit = false>
+          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false, bool kSplit = false, bool kHalf = false>
 void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
             uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
             const Sideband &sb = Sideband{}) {
     const uint64_t tiles = (n + kBlock - 1) / kBlock;
     const uint64_t grid = (uint64_t)grid_per_cu * cus;
     const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16, kSplit>),
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16, kSplit, kHalf>),
                        dim3(g), dim3(kBlock), 0,
                        stream, *T, *in, n, results, verdicts, st, sb);
 }
@@ -1048,7 +1085,10 @@ bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const
         if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
         else launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     } else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on) {
-        if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        // decision lines read half-first when the compiler chose it (choose_dt_half: configs[1]-like epochs)
+        if (T->dt_half && d16_big())
+            launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+        else if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
         else launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
     }
     // with per-list part counts (16 KiB of LDS) a 4096-entry word cache and a 256-entry IPv6 group cache: same-box

@@ -177,6 +177,7 @@ void tables_io(IO &io, M &h) {  // HostTables fields, in one order for both dire
     io.vec(h.d16);
     io.pod(h.d16_on);
     io.pod(h.d16_permille);
+    io.pod(h.dt_half);
     io.pod(h.n_lists);
     io.pod(h.n_entries);
     io.pod(h.n_long_entries);
@@ -398,6 +399,7 @@ bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std
         if (!b_free) return bad("IPv6 bucket table without a free bucket");
     }
     if (overflowed != h.n_overflow_groups || (overflowed && h.levels.empty())) return bad("IPv6 overflow groups");
+    if (h.dt_half > 1) return bad("decision-line read form");
     // incremental-commit state
     if (inc.valid) {
         if (inc.list_refs.size() != L) return bad("list reference counts");

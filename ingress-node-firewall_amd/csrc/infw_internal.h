@@ -226,6 +226,7 @@ struct HostTables {
     std::vector<uint64_t> d16;           // d16_on: n_slots << 16 /16 words in front of DIR-24-8 (infw_tables.h)
     uint32_t d16_on = 0;
     uint32_t d16_permille = 0;           // of the /16s holding a prefix longer than /16, those with an inline word
+    uint32_t dt_half = 0;                // the kernel reads decision lines half-first (choose_dt_half)
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
@@ -256,6 +257,7 @@ uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *run
 // Decide whether the epoch gets /16 words (INFW_D16=0/1 forces) and build them; n_short_wide of the n_short
 // <= /32 prefixes are /20 or shorter.
 void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide);
+uint32_t choose_dt_half(const HostTables &h);
 
 // short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
 int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,

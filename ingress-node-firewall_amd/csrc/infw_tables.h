@@ -187,6 +187,7 @@ struct infw_dev_tables {
     const struct infw_dt_line *dxr_lines;
     const uint64_t *d16;       // d16_on: n_slots << 16 words in front of DIR-24-8 (INFW_D16_*)
     uint32_t d16_on;
+    uint32_t dt_half;          // read decision lines half-first (the second 32 B only where needed; choose_dt_half)
     uint32_t split;            // classify in two phases (LPM -> per-packet decision-line address; then the decision
                                // lines as independent gathers): epochs whose entry lines span GiBs (classify.hip)
 };

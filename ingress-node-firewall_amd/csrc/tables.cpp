@@ -1420,6 +1420,7 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.n_buckets = groups.size();
     }
     phase("buckets");
+    out.dt_half = choose_dt_half(out);
     if (inc) {
         // the buffers incremental commits append to get the device images' 25 % slack on the host too, so
         // the first commits after a compile do not copy a 30-MB vector to grow it by one rule list
@@ -1444,6 +1445,18 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     }
     phase("slack+inc");
     return 0;
+}
+
+uint32_t choose_dt_half(const HostTables &h) {
+    // the kernel's decision-line reads (infw_dev_tables.dt_half): the first 32 B, then the second half only where
+    // needed, when nearly every entry line is a compact leaf of <= 9 segments (answered by its first half: configs[1],
+    // same-box A/B 1.107 -> 1.020 ms); else the whole line at once (a wave waits for the dependent second half
+    // whenever one of its lanes needs it: configs[2] and [4] 0.2-0.5 % slower reading halves, profiles/r04hf)
+    if (const char *e = getenv("INFW_DT_HALF")) return atoi(e) ? 1u : 0u;
+    uint64_t short_lines = 0;
+    for (const infw_dt_line &l : h.dte)
+        short_lines += (l.w[0] & INFW_DT_COMPACT) && !(l.w[0] & INFW_DT_ROOT) && (l.w[0] & 0xFFu) <= 9;
+    return !h.dte.empty() && short_lines * 100 >= (uint64_t)h.dte.size() * 95 ? 1u : 0u;
 }
 
 uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs) {

@@ -123,7 +123,7 @@ class TableInfo(C.Structure):
                 ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32),
                 ("device_ms_max", C.c_double), ("n_device_slots", C.c_uint32), ("imported", C.c_uint32),
                 ("d16", C.c_uint32), ("d16_permille", C.c_uint32), ("split", C.c_uint32),
-                ("pad1", C.c_uint32), ("reserved", C.c_uint64 * 12)]
+                ("dt_half_reads", C.c_uint32), ("reserved", C.c_uint64 * 12)]
 
 
 assert C.sizeof(LpmIpKeySt) == 24 and C.sizeof(RuleTypeSt) == 12

@@ -41,6 +41,47 @@ def test_parity_configs(cfg, n, npfx, ntmpl):
     assert acts[1] + acts[2] > 0
 
 
+@pytest.mark.parametrize("half", ["0", "1"])
+def test_parity_dt_half_reads(monkeypatch, half):
+    """Decision lines read half-first (INFW_DT_HALF=1: the first 32 B, the second half only for roots, u32 leaves and
+    compact leaves of > 9 segments past their key 8; the compiler's choice for configs[1]-like epochs, run by the
+    /16-word kernel shape) or whole (0): bit-exact either way on configs[1]; on configs[2] (100k) and [4] (20k) rule
+    lists in that shape (/16 words forced, no per-list part counts: leaves of up to 20 segments, root entries); and on
+    an IPv4 table of rule values with ids past 127 and actions outside {1, 2} (u32-form leaves)."""
+    import random
+    import struct
+    import orc
+    from test_compiler_cpu import _val
+    from test_incremental_cpu import _packets_for
+    monkeypatch.setenv("INFW_DT_HALF", half)
+    r = check_cfg(W.CFG1_V4_10K, 1 << 18)
+    assert r["clf"].info()["dt_half_reads"] == int(half) and r["clf"].info()["d16"] == 1
+    assert_parity(r, f"cfg1-dt-half{half}")
+    monkeypatch.setenv("INFW_D16", "1")
+    monkeypatch.setenv("INFW_DT_ADAPT", "0")
+    for cfg, npfx, ntmpl in ((W.CFG2_MIXED_1M, 100000, 512), (W.CFG4_ADVERSARIAL, 20000, 64)):
+        r = check_cfg(cfg, 1 << 18, npfx, ntmpl)
+        assert r["clf"].info()["dt_half_reads"] == int(half) and r["clf"].info()["d16"] == 1
+        assert_parity(r, f"cfg{cfg}-dt-half{half}")
+    rng = random.Random(21)
+    ents = []
+    for i in range(3000):
+        L = rng.choice([16, 18, 20, 24, 28, 32])
+        a = rng.getrandbits(32) & (~((1 << (32 - L)) - 1) & 0xFFFFFFFF)
+        ents.append((struct.pack("<II", L + 32, rng.choice([3, 4])) + a.to_bytes(4, "big") + bytes(12), _val(rng, i)))
+    clf = infw.Classifier(devices=[0])
+    m = orc.OracleMap()
+    for k, v in ents:
+        assert clf.update_rc(infw.LpmIpKeySt.from_buffer_copy(k), infw.RulesValSt.from_buffer_copy(v)) == m.update(k, v)
+    clf.commit()
+    assert clf.info()["dt_half_reads"] == int(half) and clf.info()["d16"] == 1
+    hdr, cap, pl, ifx = _packets_for([k for k, _ in ents], rng, 8)
+    want, _, _, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    got, _ = gpu_run(clf, SoaBatch.from_tuples(W.pack_frames(hdr, cap, pl, ifx), torch.device("cuda", 0)), len(ifx))
+    assert np.array_equal(got, want)
+    assert (want != 0).mean() > 0.3
+
+
 def test_parity_cfg2_full_table_subsample():
     """configs[2] at its full 1M-prefix table, 256k packets from the middle of a shard."""
     r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, start=(1 << 27) + 12345)

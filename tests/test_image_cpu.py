@@ -132,7 +132,7 @@ _TABLES = [("if_keys", "v", 4), ("if_slot", "v", 4), ("if_mult", "p", 4), ("if_s
            ("n_buckets", "p", 8), ("n_overflow_groups", "p", 8), ("b2n", "p", 8), ("wild", "v", 4), ("n_wild", "p", 4),
            ("levels", "v", 1), ("desc", "v", 8), ("rules", "v", 8), ("dte", "v", 64), ("dtl", "v", 64),
            ("dt_plog2", "p", 4), ("dt_pl", "v", 4), ("dxr_idx", "v", 4), ("dxr_lines", "v", 64), ("d16", "v", 8),
-           ("d16_on", "p", 4), ("d16_permille", "p", 4), ("n_lists", "p", 4), ("n_entries", "p", 8),
+           ("d16_on", "p", 4), ("d16_permille", "p", 4), ("dt_half", "p", 4), ("n_lists", "p", 4), ("n_entries", "p", 8),
            ("n_long_entries", "p", 8)]
 
 
