@@ -30,9 +30,12 @@ $(OBJ)/classify.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 # layout — image.cpp's field order, infw_internal.h's HostTables / IncState, incremental.cpp's state — is in it)
 BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
                 $(SRC)/image.cpp $(SRC)/infw_internal.h $(SRC)/incremental.cpp
+# The flags part is fixed when the Makefile is read (abi.cpp's, which compiles the id in): a target-specific HIPFLAGS
+# of whichever target first needs the header (classify.hip.o's, abi.cpp.o's, the sanitizer objects') must not change it.
+BUILDID_FLAGS := $(HIPFLAGS) -I$(OBJ)
 $(OBJ)/infw_build_id.h: $(BUILDID_SRCS) Makefile
 	@mkdir -p $(OBJ)
-	@printf '#define INFW_BUILD_ID "%s"\n' "$$( (cat $(BUILDID_SRCS); echo '$(HIPFLAGS) $(EXTRA) $(ARCH)') | sha256sum | cut -c1-16)" > $@.tmp
+	@printf '#define INFW_BUILD_ID "%s"\n' "$$( (cat $(BUILDID_SRCS); echo '$(BUILDID_FLAGS) $(EXTRA) $(ARCH)') | sha256sum | cut -c1-16)" > $@.tmp
 	@cmp -s $@.tmp $@ && rm -f $@.tmp || mv $@.tmp $@
 $(OBJ)/abi.cpp.o: $(OBJ)/infw_build_id.h
 $(OBJ)/abi.cpp.o: HIPFLAGS += -I$(OBJ)
