@@ -28,7 +28,7 @@ $(OBJ)/classify.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 # bench.py only attaches a profile's PMC figures to a line when the profile was taken on the same build id
 # (and a table image is accepted only by a library of the same build id, so every source that defines the serialised
 # layout — image.cpp's field order, infw_internal.h's HostTables / IncState, incremental.cpp's state — is in it)
-BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
+BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_launch.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
                 $(SRC)/image.cpp $(SRC)/infw_internal.h $(SRC)/incremental.cpp
 # The flags part is fixed when the Makefile is read (abi.cpp's, which compiles the id in): a target-specific HIPFLAGS
 # of whichever target first needs the header (classify.hip.o's, abi.cpp.o's, the sanitizer objects') must not change it.
@@ -103,10 +103,26 @@ $(ASAN_DIR)/asan_abi: tools/asan_abi.cpp $(ASAN_DIR)/libinfw.so
 	g++ $(ASAN_FLAGS) -o $@ tools/asan_abi.cpp -L$(ASAN_DIR) -linfw -Wl,-rpath,'$$ORIGIN'
 asan-host: $(ASAN_DIR)/asan_abi $(ASAN_DIR)/infw_loader_test
 
+# ThreadSanitizer build of the same host sources and tools/tsan_abi.cpp, which runs the C ABI's threading contract
+# (include/infw.h "threads": a control-plane thread committing epochs while reader threads walk, read and introspect)
+# on a host-only context.  tests/test_threads_cpu.py runs it.
+TSAN_DIR   := $(OBJ)/tsan
+TSAN_FLAGS := -std=c++17 -g -O1 -fPIC -fsanitize=thread -fno-omit-frame-pointer -Iinclude -I$(OBJ) -I/opt/rocm/include \
+              -D__HIP_PLATFORM_AMD__
+TSAN_OBJS  := $(patsubst $(SRC)/%,$(TSAN_DIR)/%.o,$(ASAN_SRCS))
+$(TSAN_DIR)/%.o: $(SRC)/% $(HDRS) $(OBJ)/infw_build_id.h
+	@mkdir -p $(TSAN_DIR)
+	g++ $(TSAN_FLAGS) -c $< -o $@
+$(TSAN_DIR)/libinfw.so: $(TSAN_OBJS) $(HIP_OBJS)
+	g++ -shared -fsanitize=thread -o $@ $^ -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+$(TSAN_DIR)/tsan_abi: tools/tsan_abi.cpp $(TSAN_DIR)/libinfw.so
+	g++ $(TSAN_FLAGS) -o $@ tools/tsan_abi.cpp -L$(TSAN_DIR) -linfw -Wl,-rpath,'$$ORIGIN'
+tsan-host: $(TSAN_DIR)/tsan_abi
+
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build
 
-.PHONY: all clean resource-usage asm asan asan-host cachesim patch_bench
+.PHONY: all clean resource-usage asm asan asan-host tsan-host cachesim patch_bench
 
 # host model of the L2 behaviour of the table walk (layout experiments; tools/cachesim.cpp)
 cachesim: $(OUT)/libinfw_workload.so

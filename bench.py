@@ -34,6 +34,15 @@ shard is identical at any GPU count (weak scaling).  The table is compiled once
                        (infw_debug_walk) and the counters go through the same
                        StatsExchange over gloo.  Checks the launcher, sharding
                        and exchange; the line says it is not a measurement.
+  --in-process         the library's own multi-GPU shape: ONE process, ONE
+                       context over N device slots (the table compiled once and
+                       published to every slot), one host thread and HIP stream
+                       per slot classifying its shard, the counters summed per
+                       rule over the slots (infw_stats_read_all, the per-CPU
+                       read of statistics.go:126-157).  --slots-on-gpu0 puts all
+                       N slots on device 0 (a one-GPU rehearsal of the shape).
+  --opt NAME=VALUE     a per-context option (include/infw.h infw_set_option) for
+                       every context the bench creates (A/B runs of table forms).
 """
 from __future__ import annotations
 
@@ -164,10 +173,23 @@ def parse(argv=None):
     ap.add_argument("--from-frames", type=int, default=0, metavar="STRIDE",
                     help="packer-fed step: raw frames resident in HBM at this stride (e.g. 128) -> infw_pack_frames_c "
                          "-> infw_classify_c, both timed (implies --layout compact)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one process, one context over N device slots, a host thread + stream per slot")
+    ap.add_argument("--slots-on-gpu0", action="store_true",
+                    help="with --in-process: every slot on device 0 (rehearsal of the N-slot shape on one GPU)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="per-context option (include/infw.h) for every context this bench creates")
     ap.add_argument("--fused", action="store_true",
                     help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
                          "no SoA batch written or read; checked untimed against the packer path's results")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    args.options = {}
+    for o in args.opt:
+        name, _, val = o.partition("=")
+        if not name or not val:
+            ap.error(f"--opt {o!r}: NAME=VALUE")
+        args.options[name] = int(val)
+    return args
 
 
 def free_port() -> int:
@@ -182,6 +204,10 @@ def main(argv=None):
     (or --spawn) starts N rank processes with torch.multiprocessing's spawn start method: fresh interpreters, so
     nothing of the parent's state — which never touches the GPU — is inherited, and each rank binds its own GPU."""
     args = parse(argv)
+    if args.in_process:
+        if args.host_walk:
+            return run_in_process_host_walk(args, args.gpus or 1)
+        return run_in_process(args, args.gpus or 1)
     if "WORLD_SIZE" in os.environ:
         world = int(os.environ["WORLD_SIZE"])
         if args.gpus is not None and args.gpus != world:
@@ -317,7 +343,7 @@ def run_host_walk(args, world, rank, use_dist, log):
     if use_dist:
         dist.init_process_group("gloo")
     wl = W.Workload(args.cfg, n_prefixes=args.prefixes or 20000, n_templates=args.templates or 64)
-    clf = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 16)
+    clf = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 16, options=args.options)
     how, setup_s = share_tables(args, clf, wl, rank, world, use_dist, log)
     if args.global_packets:
         start, end = shard_range(args.global_packets, rank, world)
@@ -397,7 +423,7 @@ def run_rank(args):
     wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
     if args.uniform:
         wl.uniform_sources()
-    clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16)
+    clf = infw.Classifier(devices=[local], max_entries=wl.n_entries + 16, options=args.options)
     how, setup_s = share_tables(args, clf, wl, rank, world, use_dist, log)
     commit_s = setup_s
     info = clf.info()
@@ -454,7 +480,7 @@ def run_rank(args):
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     # the device's random-line and stream rates, measured in this process just before the timed loop (same lease,
     # same device): what random_line_model prices the kernel's PMC line counts with (~0.3 s, untimed)
-    rates = None if args.no_line_rates else W.line_rates(local)
+    rates = None if args.no_line_rates else probe_line_rates(W, local, log)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
@@ -527,12 +553,10 @@ def run_rank(args):
     else:
         assert torch.equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
     digest = stats_digest(digest_block.cpu().numpy())
-    block, group, bpc = clf.launch()
-    kernel = f"classify_kernel<{block}, {group}> ({bpc} workgroups per CU)" + (
-        " (family-compact layout)" if args.layout == "compact" else "") + (
-        " + decide_kernel<512> (two-phase form)" if info.get("split") and not args.from_frames else "")
+    # the registry name of the instantiation(s) this line ran (infw_classify_variant: the library's own selector)
+    kernel = clf.variant({"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
+                          "frames": infw.INPUT_FRAMES}[args.layout])
     if args.fused:
-        kernel = "classify_kernel<768, 0> (2 workgroups per CU) (raw frames: infw_classify_frames)"
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,
                                       "results_equal_packer_path": fused_check}}
     elif args.from_frames:
@@ -676,6 +700,202 @@ def run_rank(args):
     clf.stats_bind(0, None)
     if use_dist:
         dist.destroy_process_group()
+
+
+def probe_line_rates(W, ordinal, log):
+    """The device's random-line and stream rates (workload.hip), or None when the probe cannot allocate its 2-GiB
+    buffers beside the tables (a rank whose device is full reports no random_line_model, not a crash)."""
+    import infw
+    try:
+        return W.line_rates(ordinal)
+    except infw.InfwError as e:
+        log(f"[bench] line-rate probe skipped: {e}")
+        return None
+
+
+def _slot_shard(args, s, n_slots):
+    """Packets [start, start + n) of slot s: a fixed job's shard_range, or a fixed batch per slot (weak)."""
+    if args.global_packets:
+        a, b = shard_range(args.global_packets, s, n_slots)
+        return a, b - a
+    return s * args.batch, args.batch
+
+
+def run_in_process(args, n_slots):
+    """The library's own multi-GPU shape (how a cgo daemon would drive it): one context over N device
+    slots — the table compiled once and published to every slot by infw_table_commit (one host thread per slot) —
+    and one host thread with its own HIP stream per slot classifying that slot's shard, K steps back to back.  Each
+    slot's counters land in its own statistics slot (kernel.c:36-41's per-CPU slots); the reader sums them per rule
+    with infw_stats_read_all (statistics.go:126-157), so no collective is involved.  The timed region is bracketed
+    by a thread barrier and a synchronize of every device; value = packets of all slots / that time."""
+    import threading
+
+    import numpy as np
+    import torch
+
+    import infw
+    from infw import workloads as W
+    from infw.batch import SoaBatch
+
+    def log(*a):
+        print(*a, file=sys.stderr, flush=True)
+
+    have = torch.cuda.device_count()
+    devices = [0] * n_slots if args.slots_on_gpu0 else list(range(n_slots))
+    if max(devices) >= have:
+        sys.exit(f"bench.py --in-process: {n_slots} slots need {max(devices) + 1} device(s), {have} visible")
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes, n_templates=args.templates)
+    if args.uniform:
+        wl.uniform_sources()
+    clf = infw.Classifier(devices=devices, max_entries=wl.n_entries + 16, options=args.options)
+    t0 = time.time()
+    wl.load_into(clf, order=wl.shuffled_order() if args.key_order == "shuffled" else None)
+    clf.commit()
+    info = clf.info()
+    setup_s = time.time() - t0
+    log(f"[bench] in-process: {n_slots} slot(s) on device(s) {devices}, {wl.n_entries} entries, tables compiled once "
+        f"and published to every slot in {setup_s:.1f}s (slowest slot {info['device_ms_max']:.0f} ms)")
+    shards = [_slot_shard(args, s, n_slots) for s in range(n_slots)]
+    batches, results, streams = [], [], []
+    for s, (start, n) in enumerate(shards):
+        dev = torch.device("cuda", devices[s])
+        b = SoaBatch.empty(max(n, 1), dev).slice(0, n)
+        if n:
+            wl.gen_device(b, start=start, dev_ordinal=devices[s])
+        batches.append(b)
+        results.append(torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n])
+        streams.append(torch.cuda.Stream(device=dev))
+    for d in set(devices):
+        torch.cuda.synchronize(d)
+    evs = [[tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(args.steps)]
+           for _ in range(n_slots)]
+    errors = []
+
+    def slot_thread(s, steps, gate, timed):
+        try:
+            torch.cuda.set_device(devices[s])
+            gate.wait()
+            for k in range(steps):
+                if timed:
+                    evs[s][k][0].record(streams[s])
+                if shards[s][1]:
+                    clf.classify(batches[s], results=results[s], dev=s, stream=streams[s])
+                if timed:
+                    evs[s][k][1].record(streams[s])
+        except BaseException as e:  # surfaced by the main thread
+            errors.append(e)
+            gate.abort()
+
+    def run(steps, timed):
+        gate = threading.Barrier(n_slots + 1)
+        th = [threading.Thread(target=slot_thread, args=(s, steps, gate, timed)) for s in range(n_slots)]
+        for t in th:
+            t.start()
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        gate.wait()
+        ts = time.perf_counter()
+        for t in th:
+            t.join()
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        if errors:
+            raise errors[0]
+        return time.perf_counter() - ts
+
+    clf.stats_reset()
+    run(args.warmup, False)
+    warm = clf.stats_read_all()
+    clf.stats_reset()
+    elapsed = run(args.steps, True)
+    total = clf.stats_read_all()  # summed per rule over the slots (infw_stats_read_all)
+    if args.warmup:
+        assert not (warm % args.warmup).any(), "warmup steps' counters differ"
+        digest_block = warm // args.warmup
+        assert np.array_equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
+    else:
+        assert not (total % max(args.steps, 1)).any(), "timed steps' counters differ"
+        digest_block = total // max(args.steps, 1)
+    job = sum(n for _, n in shards)
+    kern = [sum(e[0].elapsed_time(e[1]) for e in evs[s]) / max(args.steps, 1) for s in range(n_slots)]
+    out = {
+        "metric": METRIC, "value": round(job * args.steps / elapsed / 1e6, 2), "unit": "Mpps",
+        "n_gpus": len(set(devices)), "mode": "in-process", "device_slots": n_slots, "rccl_world_size": None,
+        "build_id": infw.build_id(), "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong" if args.global_packets else "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload_key": workload_key(args.cfg, args.templates, args.prefixes), "prefixes": wl.n_entries,
+                   "rule_lists": info["n_lists"], "global_batch": job,
+                   "parallelism": f"{n_slots} device slot(s) of one context on device(s) {sorted(set(devices))}, "
+                                  "one host thread + stream each, counters summed per rule over slots",
+                   "packets_counted_in_stats": int(digest_block[:, 0].sum() + digest_block[:, 2].sum()),
+                   "stats_digest": stats_digest(digest_block),
+                   "tables": {"setup_s": round(setup_s, 2), "device_ms_max": round(info["device_ms_max"], 1),
+                              "n_device_slots": info["n_device_slots"]}},
+        "kernel": clf.variant(infw.INPUT_SOA),
+        "per_slot": [{"slot": s, "device": devices[s], "packets_per_step": shards[s][1],
+                      "kernel_ms_avg": round(kern[s], 4)} for s in range(n_slots)],
+    }
+    print(json.dumps(out), flush=True)
+    clf.close()
+
+
+def run_in_process_host_walk(args, n_slots):
+    """TEST ONLY (--in-process --host-walk): the in-process shape on a CPU box — one host-only context, one host
+    thread per slot walking its shard through the compiled host image (infw_debug_walk, which may run on many
+    threads at once), the slots' counters summed per rule.  The digest equals the rank path's for the same job."""
+    import threading
+
+    import numpy as np
+
+    import infw
+    from infw import workloads as W
+    wl = W.Workload(args.cfg, n_prefixes=args.prefixes or 20000, n_templates=args.templates or 64)
+    clf = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 16, options=args.options)
+    wl.load_into(clf, order=wl.shuffled_order() if args.key_order == "shuffled" else None)
+    clf.commit()
+    shards = []
+    for s in range(n_slots):
+        if args.global_packets:
+            a, b = shard_range(args.global_packets, s, n_slots)
+            shards.append((a, b - a))
+        else:
+            shards.append((s * min(args.batch, 1 << 16), min(args.batch, 1 << 16)))
+    slots = [np.zeros((1024, 4), np.uint64) for _ in range(n_slots)]
+    errors = []
+
+    def slot_thread(s):
+        try:
+            start, n = shards[s]
+            if n:
+                t = wl.tuples(start, n)
+                for _ in range(max(args.steps, 1)):
+                    slots[s] += host_counters(clf.debug_walk(t), t[:, 5])
+        except BaseException as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=slot_thread, args=(s,)) for s in range(n_slots)]
+    ts = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    elapsed = time.perf_counter() - ts
+    if errors:
+        raise errors[0]
+    total = sum(slots)
+    assert not (total % max(args.steps, 1)).any()
+    block = total // max(args.steps, 1)
+    job = sum(n for _, n in shards)
+    print(json.dumps({
+        "metric": METRIC + " [host-walk selftest: not a measurement]", "value": round(job * args.steps / elapsed / 1e6, 4),
+        "unit": "Mpps", "valid_measurement": False, "n_gpus": 0, "mode": "in-process", "device_slots": n_slots,
+        "steps": args.steps, "scaling": "strong" if args.global_packets else "weak", "build_id": infw.build_id(),
+        "config": {"workload_key": workload_key(args.cfg, args.templates, args.prefixes), "prefixes": wl.n_entries,
+                   "global_batch": job, "packets_counted_in_stats": int(block[:, 0].sum() + block[:, 2].sum()),
+                   "stats_digest": stats_digest(block)},
+        "per_slot": [{"slot": s, "packets_per_step": shards[s][1]} for s in range(n_slots)]}), flush=True)
 
 
 def cpu_baseline(args, wl, results, n, start=0):

@@ -12,10 +12,18 @@
  *   - return 0 on success or a negative errno (-EINVAL, -ENOENT, -EEXIST,
  *     -ENOSPC, -ENOMEM, -ENODEV, -EIO);
  *   - opaque handle, caller-owned buffers, no callbacks;
- *   - control-plane calls (table_*, commit, stats_reset) are externally
- *     serialised, like ebpfsyncer.go:62,72-73 (e.mu); infw_classify may run
- *     concurrently on other threads/streams and each batch observes exactly
- *     one committed table epoch.
+ *   - threads: control-plane calls (infw_table_*, infw_table_commit,
+ *     infw_table_import/export, infw_stats_reset, infw_set_option,
+ *     infw_set_launch, infw_debug_lookup_set, infw_debug_keys_clear) are
+ *     externally serialised, like ebpfsyncer.go:62,72-73 (e.mu).  The data
+ *     path and the readers — infw_classify*, infw_pack_frames*,
+ *     infw_events_capture, infw_stats_read*, infw_table_info,
+ *     infw_debug_walk, infw_debug_keys_read, infw_classify_variant — may run
+ *     on any number of other threads concurrently with them and with each
+ *     other; each batch observes exactly one committed table epoch;
+ *   - the library reads no environment variable: everything that selects a
+ *     table form or a kernel is a per-context option (infw_set_option), and
+ *     no option changes a result word, a verdict or a counter.
  *
  * No torch types, no HIP types: device buffers and streams are plain pointers.
  */
@@ -193,7 +201,6 @@ typedef struct infw_ctx infw_ctx;
                                     /* image is always kept (incremental       */
                                     /* commits patch it; infw_debug_walk reads) */
 #define INFW_F_FULL_COMMIT 0x4u     /* every commit recompiles the whole epoch  */
-                                    /* (env INFW_FULL_COMMIT=1 does the same)   */
 int infw_create(infw_ctx **out, const int *hip_devices, int n_dev,
                 uint32_t max_entries, uint32_t flags);
 void infw_destroy(infw_ctx *ctx);
@@ -266,15 +273,54 @@ int infw_classify_c(infw_ctx *ctx, int dev, const struct infw_batch_soa_c *in, u
 int infw_soa_compact(infw_ctx *ctx, int dev, const struct infw_batch_soa *in, uint64_t n,
                      uint32_t *saddr4, uint8_t *v6tail, void *stream);
 
-/* Launch shape of the classify kernel (tuning; defaults 768 / 0 / 2 = 24    */
-/* waves per CU, or the INFW_BLOCK, INFW_SCAN_GROUP, INFW_BLOCKS_PER_CU       */
-/* environment variables): block 256|512|768 threads (other multiples of 64  */
-/* run as 512 x 3); scan_group 0 = first-match decision tables, or 1|4|8 =   */
-/* one-lane-per-rule ballot scan with that many packets in flight;           */
-/* blocks_per_cu resident workgroups per CU.                                  */
+/* Launch shape of the classify kernel (default 768 / 0 / 2 = 24 waves per CU). */
+/* scan_group 0 = first-match decision tables in one of the shapes           */
+/* (block x blocks_per_cu) 768x2, 512x2, 512x3, 512x4, 256x6; scan_group      */
+/* 1|4|8 = the one-lane-per-rule ballot scan (kernel.c:222-258 in rule order) */
+/* with that many packets in flight, 512x3 or 256x6.  -EINVAL for any other   */
+/* shape.  The family-compact layout runs non-default shapes as decision       */
+/* tables 512x3; frames and sideband launches have fixed shapes.               */
 int infw_set_launch(infw_ctx *ctx, int block, int scan_group, int blocks_per_cu);
 /* The launch shape infw_classify uses (default or set above; bench reporting). */
 int infw_get_launch(infw_ctx *ctx, int *block, int *scan_group, int *blocks_per_cu);
+
+/* Per-context options.  Each selects among bit-exact forms of the same table */
+/* epoch (full compiles read them), how the classify launch reads it, or      */
+/* tracing — results, verdicts and counters never depend on them.  value -1   */
+/* means "chosen per epoch" where an option has that.  -EINVAL for an unknown */
+/* name or a value out of range (nothing changes then).                       */
+/*   short_table      -1 auto (DIR-24-8 while ifindexes x 128 MiB <= 4 GiB),   */
+/*                    0 DIR-24-8, 1 compressed 16-8-8 (next full compile)      */
+/*   d16              -1 auto, 0 off, 1 on: /16 words in front of DIR-24-8      */
+/*   dt_half          -1 auto, 0 off, 1 on: half-first decision-line reads      */
+/*   dt_parts         0 auto, or 1|2|4|8|16 value parts per (list, class)        */
+/*   dt_adapt         1 per-list part counts (<= 4096 lists), 0 uniform parts    */
+/*   dt_budget_mb     64..1048576 (2048): entry lines of one image at most        */
+/*   compile_threads  0 hardware threads (<= 16), or 1..16                        */
+/*   split            -1 auto, 0 off, 1 on: two-phase classify (many lists)       */
+/*   split_min_mb     0..1048576 (1024): auto splits past this many MiB of lines  */
+/*   stat_flush_tiles 1..1024 (1024): LDS counter flush period in tiles           */
+/*   trace            bit mask to stderr: 1 compile, 2 incremental patch,          */
+/*                    4 commit timing                                              */
+int infw_set_option(infw_ctx *ctx, const char *name, int64_t value);
+int infw_get_option(infw_ctx *ctx, const char *name, int64_t *value);
+/* Name of option i (0-based), NULL past the last.                             */
+const char *infw_option_name(int i);
+
+/* Which kernel instantiation(s) a launch would run (introspection; nothing is */
+/* launched, no device needed — host-only contexts answer from their image).  */
+/* input: INFW_INPUT_*; flags: INFW_VARIANT_EVENTS for an infw_classify_ex     */
+/* event stream (the debug sideband follows infw_debug_lookup_set).  name is a */
+/* registry name (infw_kernel_variant_name); two-phase launches name both      */
+/* kernels joined by '+'.  -ERANGE when cap is too small.                      */
+#define INFW_INPUT_SOA 0
+#define INFW_INPUT_COMPACT 1
+#define INFW_INPUT_FRAMES 2
+#define INFW_VARIANT_EVENTS 0x1u
+int infw_classify_variant(infw_ctx *ctx, int dev, int input, uint32_t flags, char *name, size_t cap);
+/* Registry of every kernel instantiation the library launches: name of entry */
+/* i (0-based), NULL past the last.                                            */
+const char *infw_kernel_variant_name(int i);
 
 /* Frame headers -> SoA tuples on the device (the packer of the batch format  */
 /* above, run as a kernel over frames already in HBM).  Asynchronous.          */
@@ -458,12 +504,11 @@ struct infw_table_info {
     uint64_t dead_lists;       /* compiled lists no entry references (GC'd by */
                                /* the next full compile)                      */
     char full_reason[48];      /* why the last full compile was needed        */
-    uint64_t v6_slot_buckets;  /* != 0: IPv6 groups in the two-choice slot    */
-                               /* form, this many 64-B buckets (else one group */
-                               /* per bucket at <= 1/8 load)                   */
+    uint64_t reserved0;        /* zero (ABI 3: the removed two-choice IPv6     */
+                               /* slot form)                                   */
     uint32_t short_mode;       /* <= /32 key space: 0 DIR-24-8, 1 compressed   */
-                               /* 16-8-8, 2 none, 3 range form (/16 chunks)    */
-    uint32_t dxr_lines;        /* range lines of the range form                */
+                               /* 16-8-8, 2 none                               */
+    uint32_t reserved1;        /* zero (ABI 3: the removed range form)         */
     /* ABI 3: commit timing per device slot (the slots upload / patch in        */
     /* parallel, one host thread each) and room to grow without another break.  */
     double device_ms_max;      /* slowest slot's upload / patch of the last     */
@@ -477,9 +522,9 @@ struct infw_table_info {
     uint32_t split;            /* 1: the epoch classifies in two phases (LPM   */
                                /* -> decision-line address per packet, then   */
                                /* the decision lines as independent gathers):  */
-                               /* many distinct rule lists (INFW_SPLIT=0/1)    */
+                               /* many distinct rule lists (option split)      */
     uint32_t dt_half_reads;    /* 1: decision lines read half-first (nearly all */
-                               /* compact leaves of <= 9 segments; INFW_DT_HALF) */
+                               /* compact leaves of <= 9 segments; dt_half)    */
     uint64_t reserved[12];     /* zero; future fields come out of this         */
 };
 #define INFW_COMMIT_FULL 0u        /* compile + upload of a fresh image           */
@@ -497,7 +542,9 @@ int infw_debug_walk(infw_ctx *ctx, const uint32_t *tuples, uint64_t n, uint32_t 
 const char *infw_last_error(void);
 /* ABI version (bumped on incompatible change).  3: struct infw_table_info     */
 /* grew (and now ends in reserved space), infw_build_id, table export/import. */
-#define INFW_ABI_VERSION 3
+/* 4: per-context options replace environment variables, infw_set_launch      */
+/* accepts only the registered shapes, kernel-variant introspection.          */
+#define INFW_ABI_VERSION 4
 int infw_abi_version(void);
 /* Identity of the code this library was built from: a hash of the kernel and */
 /* table-layout sources and the flags they were compiled with (Makefile).       */

@@ -17,13 +17,16 @@
 //      summed per wavefront for the leading counter slot, the rest go to LDS
 //      atomics (u32 packets, u64 bytes per rule id), flushed with one u64
 //      atomic per touched counter when the workgroup retires.
+#include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/infw.h"
 #include "infw_tables.h"
+#include "infw_launch.h"
 
 namespace {
 
@@ -35,7 +38,6 @@ constexpr uint32_t kBigLen = 1u << 20;                      // frames this long 
 constexpr unsigned long long kBytesMask = (1ull << 40) - 1;  // bytes field of a packed LDS counter
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kIfLds = 256;  // ifindex map entries mirrored in LDS
-constexpr int kC24LogDefault = 10;  // per-workgroup LDS cache of plain DIR-24-8 words: 1 << kC24Log entries
 // word tags of the IPv6 group cache: tag ^ C_j in word j (distinct, so an all-zero entry never validates)
 constexpr uint32_t kB6C0 = 0x00000001u, kB6C1 = 0x5bd1e995u, kB6C2 = 0x9e3779b9u, kB6C3 = 0xc2b2ae35u;
 
@@ -80,7 +82,7 @@ __device__ __forceinline__ uint32_t short_lookup_cached(const infw_dev_tables &T
                                                         unsigned long long *s_c24) {
     if (!kCache || T.short_mode != INFW_SHORT_DIR24 || slot >= 256u)
         return kLean ? (T.short_mode == INFW_SHORT_DIR24 ? (kD16 ? infw_d16_lookup(T, slot, a32) : infw_dir24_lookup(T, slot, a32))
-                        : T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, slot, a32) : 0u)
+                        : 0u)
                      : infw_short_lookup(T, slot, a32);
     if (kD16) {  // the LDS cache holds /16 words: a cached or fetched inline word answers, else the tbl24 word
         const uint32_t key16 = slot << 16 | a32 >> 16, di = d16c_idx<kLog>(key16);
@@ -283,66 +285,6 @@ __device__ __forceinline__ uint32_t v6_finish(const infw_dev_tables &T, uint32_t
     }
 }
 
-// v6_finish over the two-choice slot form (infw_tables.h): slot 0 {h, r0} of bucket bi is loaded; slot 1 of the
-// same 64-B bucket only when slot 0 holds another group or a second record, the second bucket only when the
-// first is marked DISPLACED.
-template <bool kLean = false>
-__device__ __forceinline__ uint32_t v6_finish_b2(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
-                                                const uint32_t sa[4], uint64_t hash, uint64_t bi, u32x4 h, u32x4 r0) {
-    const uint32_t mid = infw_bswap32(sa[1]);
-    const uint64_t lo = infw_be64(sa[2], sa[3]);
-    for (int probe = 0;; probe++) {
-        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
-        if (h[0] == 0) {  // empty bucket (an emptied slot 0 keeps the bucket's DISPLACED flag)
-            if (probe || !(h[2] & INFW_B2_DISPLACED)) return 0;
-        } else if (h[0] == slot + 1 && h[1] == a32) {
-            const uint32_t nr = h[2] & 0xFFu;
-            if (nr == INFW_BUCKET_OVERFLOW) return kLean ? 0u : infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
-            if (infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
-            if (nr == 2) {
-                const u32x4 r1 = b[3];
-                if (infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo)) return r1[3] & 0x1FFFFFFu;
-            }
-            return 0;
-        } else {
-            const u32x4 h1 = b[2], r1 = b[3];
-            if (h1[0] == slot + 1 && h1[1] == a32) {  // a one-record (or overflowed) group in slot 1
-                if ((h1[2] & 0xFFu) == INFW_BUCKET_OVERFLOW)
-                    return kLean ? 0u : infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
-                return infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo) ? r1[3] & 0x1FFFFFFu : 0u;
-            }
-            if (probe || !(h[2] & INFW_B2_DISPLACED)) return 0;
-        }
-        bi = INFW_B2_INDEX(hash, T.b2n);
-        const u32x4 *b2 = reinterpret_cast<const u32x4 *>(T.btab + bi);
-        h = b2[0];
-        r0 = b2[1];
-    }
-}
-
-__device__ __forceinline__ uint32_t v6_long_dev(const infw_dev_tables &T, uint32_t slot, uint32_t a32,
-                                                const uint32_t sa[4]) {
-    if (T.b2n) return infw_v6_long(T, slot, a32, sa);
-    const uint32_t mid = infw_bswap32(sa[1]);
-    const uint64_t lo = infw_be64(sa[2], sa[3]);
-    uint64_t i = infw_bucket_hash(slot, a32) & T.bmask;
-    for (;;) {
-        const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + i);
-        const u32x4 h = b[0], r0 = b[1], r1 = b[2], r2 = b[3];
-        if (h[0] == 0) return 0;
-        if (h[0] == slot + 1 && h[1] == a32) {
-            const uint32_t nb = h[2];
-            if (nb == INFW_BUCKET_OVERFLOW) return infw_long_lookup(T, slot, (uint64_t)a32 << 32 | mid, lo);
-            // infw_v6_rec {lo u64, mid, meta}: words 0-1, 2, 3; longest record first
-            if (nb >= 1 && infw_rec_match(r0[2], (uint64_t)r0[1] << 32 | r0[0], r0[3], mid, lo)) return r0[3] & 0x1FFFFFFu;
-            if (nb >= 2 && infw_rec_match(r1[2], (uint64_t)r1[1] << 32 | r1[0], r1[3], mid, lo)) return r1[3] & 0x1FFFFFFu;
-            if (nb >= 3 && infw_rec_match(r2[2], (uint64_t)r2[1] << 32 | r2[0], r2[3], mid, lo)) return r2[3] & 0x1FFFFFFu;
-            return 0;
-        }
-        i = (i + 1) & T.bmask;
-    }
-}
-
 // The batch as the kernel reads it: the 16-B address layout (infw_batch_soa) or the
 // family-compact one (infw_batch_soa_c: 4 address bytes per packet + the IPv6 packets'
 // remaining 12 bytes packed at the front of a 768-B block per 64-packet group).
@@ -527,28 +469,32 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(const infw_dev_tables T,
     flush_counters();
 }
 
-// kWaves: minimum waves per SIMD the register allocation must allow (8 = four
-// 512-thread workgroups per CU; 6 leaves room for 104 SGPRs, no spills).
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kC24Log = kC24LogDefault, int kB6Log = 0,
-          bool kPrefetch = !(kAblate & 128), bool kLean = false, bool kF = false, int kV6 = 2, bool kPl = false,
-          bool kD16 = false, bool kSplit = false, bool kHalf = false>
+// One instantiation per selectable variant (the registry below):
+//   kWaves   minimum waves per SIMD the register allocation must allow (8 = four 512-thread workgroups per CU;
+//            6 leaves room for 104 SGPRs, no spills);
+//   kIn      batch form: 0 SoA tuples (infw_batch_soa), 1 family-compact (infw_batch_soa_c), 2 raw frames;
+//   kC24Log  LDS word cache of 1 << kC24Log entries (workgroups of >= 384 threads), kB6Log the IPv6 group cache
+//            (0: none);
+//   kEvents / kDebug  the deny-event and debug-lookup sidebands;
+//   kLean    the epoch has no compressed short table, overflowed IPv6 group or partial-ifindex prefix;
+//   kPl      per-list part counts mirrored in LDS; kD16 /16 words in front of DIR-24-8; kHalf half-first
+//            decision-line reads; kSplit phase 1 of the two-phase form.
+template <int kBlock, int G, int kWaves, int kIn, int kC24Log, int kB6Log, bool kEvents, bool kDebug, bool kLean,
+          bool kPl, bool kD16, bool kSplit, bool kHalf>
 __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev_tables T, const BatchIn in,
                                                           uint64_t n, uint32_t *__restrict__ results,
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
                                                           const Sideband sb) {
+    constexpr bool kC = kIn == 1, kF = kIn == 2;
     const EventSink &ev = sb.ev;
-    // IPv6 group table form: kV6 0 = one group per bucket, 1 = two-choice slots, 2 = whichever the epoch has
-    const bool b2 = kV6 == 2 ? T.b2n != 0 : kV6 == 1;
     // per-workgroup counters [rule][allow=0, deny=1], packets << 40 | bytes in one u64 (one LDS atomic per update):
     // only frames shorter than kBigLen take this path and the workgroup flushes every kFlushTiles tiles, so
     // neither field can carry into the other (kFlushTiles * kBlock * kBigLen < 2^40)
     __shared__ unsigned long long s_c[2 * kLdsStatKeys];
     __shared__ uint32_t s_ifk[kIfLds], s_ifs[kIfLds];  // ifindex -> slot map, when it fits
-    // diagnostic 32: no LDS word cache and no IPv6 group cache, 1024: no word cache only; the 256-thread shapes
-    // (6 blocks per CU) have no LDS room for it
-    constexpr bool kCache = !(kAblate & (32 | 1024)) && kBlock >= 384;
+    // the 256-thread shapes (6 blocks per CU) have no LDS room for the word cache
+    constexpr bool kCache = kBlock >= 384;
     constexpr uint32_t kC24 = 1u << kC24Log;
     __shared__ unsigned long long s_c24[kCache ? kC24 : 1];
     if (kCache)
@@ -559,7 +505,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     // group key, so a word whose tag matches was written for the reader's own group: lanes racing on an
     // entry, torn at any 8-B granularity, can only leave words of several groups, which fail the check —
     // no access needs to be indivisible beyond 8 B.  The distinct C_j keep a zeroed entry from validating.
-    constexpr bool kB6 = kB6Log > 0 && !(kAblate & 32);
+    constexpr bool kB6 = kB6Log > 0;
     __shared__ u32x4 s_b6[kB6 ? 2u << kB6Log : 1];
     __shared__ uint32_t s_fw[kF ? kBlock / 64 : 1][kF ? 16 * kFrameWinWords : 1];  // per-wave frame windows
     // kPl: the per-list part-count words (T.n_dt_pl == INFW_DT_PL_LISTS) mirrored in LDS
@@ -610,24 +556,16 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             }
             return;
         }
-        if (i < n) {
-            if (!(kAblate & 16)) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL (16: plain, diagnostic)
-                if (with_meta) meta = __builtin_nontemporal_load(&in.meta[i]);
-                l4w = __builtin_nontemporal_load(&in.l4word[i]);
-                ifx = __builtin_nontemporal_load(&in.ifindex[i]);
-                plen = __builtin_nontemporal_load(&in.pkt_len[i]);
-                if (kC) {
-                    sa = make_uint4(__builtin_nontemporal_load(&in.saddr4[i]), 0u, 0u, 0u);
-                } else {
-                    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(sa4) + i);
-                    sa = make_uint4(t[0], t[1], t[2], t[3]);
-                }
+        if (i < n) {  // streamed once: non-temporal, keeps the tables resident in L2/MALL
+            if (with_meta) meta = __builtin_nontemporal_load(&in.meta[i]);
+            l4w = __builtin_nontemporal_load(&in.l4word[i]);
+            ifx = __builtin_nontemporal_load(&in.ifindex[i]);
+            plen = __builtin_nontemporal_load(&in.pkt_len[i]);
+            if (kC) {
+                sa = make_uint4(__builtin_nontemporal_load(&in.saddr4[i]), 0u, 0u, 0u);
             } else {
-                if (with_meta) meta = in.meta[i];
-                l4w = in.l4word[i];
-                ifx = in.ifindex[i];
-                plen = in.pkt_len[i];
-                sa = kC ? make_uint4(in.saddr4[i], 0u, 0u, 0u) : sa4[i];
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(sa4) + i);
+                sa = make_uint4(t[0], t[1], t[2], t[3]);
             }
         }
     };
@@ -646,14 +584,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     };
     uint32_t n_meta = 0, n_l4w = 0, n_ifx = 0, n_plen = 0;
     uint4 n_sa = make_uint4(0, 0, 0, 0);
-    // compact + prefetch: the meta word runs two tiles ahead, so the next tile's tail loads can be issued a
+    // compact: the meta word runs two tiles ahead, so the next tile's tail loads can be issued a
     // whole tile early like the rest of its tuple (issued with the tile's own table loads, the tails' HBM
     // latency would hold back the in-order return of the bucket probes)
     uint32_t n_meta2 = 0, n_t0 = 0, n_t1 = 0, n_t2 = 0;
     {
         const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
         load_tuple(i0, n_meta, n_l4w, n_ifx, n_plen, n_sa);
-        if (kC && kPrefetch) {
+        if (kC) {
             if (i0 + stride < n) n_meta2 = __builtin_nontemporal_load(&in.meta[i0 + stride]);
             load_tail(i0, n_meta, n_t0, n_t1, n_t2);
         }
@@ -662,14 +600,13 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += stride) {
         const uint64_t i = base + threadIdx.x;
         const bool valid = i < n;
-        if (!kPrefetch && base != (uint64_t)blockIdx.x * kBlock) load_tuple(i, n_meta, n_l4w, n_ifx, n_plen, n_sa);
         uint32_t meta = valid ? n_meta : 0, l4w = n_l4w;
         const uint32_t ifx = n_ifx, plen = n_plen;
         uint4 sa = n_sa;
         if (kF) {
             const uint32_t cap = meta;  // linear length (0 past the batch: nothing is read)
             const uint64_t foff = (uint64_t)sa.y << 32 | sa.x;
-            if (kPrefetch) load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
+            load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa);
             uint32_t *wb = s_fw[threadIdx.x >> 6];
             u32x4 ch[4];
 #pragma unroll
@@ -719,14 +656,12 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             meta = et | proto << 16 | (cap > 255u ? 255u : cap) << 24;
             l4w = l4;
             sa = make_uint4(s0, s1, s2, s3);
-        } else if (kC && kPrefetch) {
+        } else if (kC) {
             sa.y = n_t0;
             sa.z = n_t1;
             sa.w = n_t2;
-        } else if (kC) {  // no prefetch (diagnostic 128): the tails load with the tile
-            load_tail(i, meta, sa.y, sa.z, sa.w);
         }
-        if (kPrefetch && !kF) {
+        if (!kF) {
             if (kC) {
                 const uint32_t m1 = n_meta2;  // tile t+1's meta, loaded one tile ago
                 load_tuple(i + stride, n_meta, n_l4w, n_ifx, n_plen, n_sa, false);
@@ -742,10 +677,6 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         const int pk = valid ? infw_parse(meta, l4w, &cls, &val) : INFW_PK_PASS_NONIP;
         uint64_t d = 0;    // ballot mode: class-list descriptor
         uint32_t lst = 0;  // decision mode: list + 1 (0: no LPM entry)
-        if (kAblate & 8) {  // diagnostic: input stream + output only
-            if (valid && results) results[i] = meta ^ l4w ^ sa.x ^ sa.y ^ sa.z ^ sa.w ^ ifx ^ plen;
-            continue;
-        }
         if (pk >= INFW_PK_V4) {
             const uint32_t sw[4] = {sa.x, sa.y, sa.z, sa.w};
             if (kDebug) {  // lookup key {prefixLen 64|160, ifindex, ip_data} (kernel.c:205-216, :292-299)
@@ -756,8 +687,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     dbg_insert(sb.dbg, key);
                 }
             }
-            uint32_t l1 = 1;  // diagnostic 1: no LPM walk, every parsed packet uses list 0
-            if (!(kAblate & 1)) {
+            uint32_t l1 = 0;
+            {
                 // ifindex -> slot (LDS copy of the open-addressed map)
                 int slot;
                 if (if_in_lds && T.if_mult) {  // collision-free placement: one probe, no loop
@@ -776,7 +707,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     slot = infw_if_slot(T, ifx);
                 }
                 l1 = 0;
-                if (slot >= 0 && !(kAblate & 512)) {
+                if (slot >= 0) {
                     // One round of table loads for the whole wave: IPv4 lanes' DIR-24-8 words
                     // and IPv6 lanes' first bucket probe are issued before either is waited
                     // for (a mixed wave would otherwise pay two dependent round trips).  IPv6:
@@ -788,8 +719,6 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                     const uint32_t key = (uint32_t)slot << 24 | a32 >> 8;
                     const uint32_t cidx = (key * 0x9E3779B1u) >> (32 - kC24Log);
                     bool need24 = !v6 && d24;
-                    const bool needx = !v6 && T.short_mode == INFW_SHORT_DXR;  // range form: index word in the round
-                    uint32_t wx = 0;
                     uint32_t sh = 0;
                     bool d16known = false;  // kD16: the LDS cache held this /16's word and it does not answer
                     const uint32_t key16 = (uint32_t)slot << 16 | a32 >> 16;
@@ -842,9 +771,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         wd = T.d16[((uint64_t)slot << 16) | (a32 >> 16)];
                     }
                     if (need24) w24 = T.tbl24[((uint64_t)slot << 24) | (a32 >> 8)];
-                    if (needx) wx = T.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
                     if (need6) {
-                        bi = b2 ? INFW_B2_INDEX(bhash >> 32, T.b2n) : bhash & T.bmask;
+                        bi = bhash & T.bmask;
                         const u32x4 *b = reinterpret_cast<const u32x4 *>(T.btab + bi);
                         bh = b[0];
                         br0 = b[1];
@@ -859,8 +787,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         }
                     }
                     if (need6) {
-                        lng = b2 ? v6_finish_b2<kLean>(T, (uint32_t)slot, a32, sw, bhash, bi, bh, br0)
-                                    : v6_finish<kLean>(T, (uint32_t)slot, a32, sw, bi, bh, br0);
+                        lng = v6_finish<kLean>(T, (uint32_t)slot, a32, sw, bi, bh, br0);
                         if (b6ok && bh[0] == (uint32_t)slot + 1 && bh[1] == a32 && bh[2] == 1u) {
                             s_b6[2 * b6idx] = u32x4{b6tag ^ kB6C0, br0[0], b6tag ^ kB6C1, br0[1]};
                             s_b6[2 * b6idx + 1] = u32x4{b6tag ^ kB6C2, br0[2], b6tag ^ kB6C3, br0[3]};
@@ -870,40 +797,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                         sh = d24_value(T, w24, a32);
                         if (!kD16 && kCache && slot < 256 && !(w24 & INFW_D24_GROUP))
                             s_c24[cidx] = 1ull << 63 | (unsigned long long)key << 31 | (uint32_t)w24;
-                    } else if (needx) {
-                        if (wx & INFW_DXR_DIRECT) {
-                            sh = wx & ~INFW_DXR_DIRECT;
-                        } else {
-                            const u32x4 *l = reinterpret_cast<const u32x4 *>(T.dxr_lines + wx);
-                            const u32x4 k0 = l[0], k1 = l[1], v2 = l[2], v3 = l[3];
-                            KeyCount kc(a32 & 0xFFFFu);
-                            kc.add(k0[0]); kc.add(k0[1]); kc.add(k0[2]); kc.add(k0[3]); kc.add(k1[0]);
-                            const uint32_t k = kc.total();  // answers in w[5..15]
-                            uint32_t r = k1[1];
-                            r = k >= 1 ? k1[2] : r;
-                            r = k >= 2 ? k1[3] : r;
-                            r = k >= 3 ? v2[0] : r;
-                            r = k >= 4 ? v2[1] : r;
-                            r = k >= 5 ? v2[2] : r;
-                            r = k >= 6 ? v2[3] : r;
-                            r = k >= 7 ? v3[0] : r;
-                            r = k >= 8 ? v3[1] : r;
-                            r = k >= 9 ? v3[2] : r;
-                            r = k >= 10 ? v3[3] : r;
-                            sh = r;
-                        }
-                    } else if (!v6 && !d24) {
-                        // range form / compressed / no short table
-                        sh = kLean ? (T.short_mode == INFW_SHORT_DXR ? infw_dxr_lookup(T, (uint32_t)slot, a32) : 0u)
-                                   : infw_short_lookup(T, (uint32_t)slot, a32);
+                    } else if (!v6 && !d24) {  // compressed / no short table
+                        sh = kLean ? 0u : infw_short_lookup(T, (uint32_t)slot, a32);
                     }
                     if (v6 && !lng) sh = short_lookup_cached<kCache, kC24Log, kLean, kD16>(T, (uint32_t)slot, a32, s_c24);
-                    l1 = lng ? lng : sh;
-                } else if (slot >= 0) {  // diagnostic 512: the sequential form (bucket round, then tbl24 round)
-                    const uint32_t a32 = infw_bswap32(sa.x);
-                    uint32_t lng = 0, sh = 0;
-                    if (pk == INFW_PK_V6 && T.n_levels) lng = v6_long_dev(T, (uint32_t)slot, a32, sw);
-                    if (!lng) sh = short_lookup_cached<kCache, kC24Log>(T, (uint32_t)slot, a32, s_c24);
                     l1 = lng ? lng : sh;
                 }
                 // an ifindex without entries of its own: prefixes shorter than the ifindex (prefixLen < 32)
@@ -928,8 +825,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         }
 
         uint32_t result = 0;
-        if (kAblate & 2) result = (uint32_t)d ^ (uint32_t)(d >> 32) ^ lst;  // diagnostic 2: no first-match stage
-        else if (G == 0 && lst) {
+        if (G == 0 && lst) {
             // the (list, class)'s own part count when the epoch has them (infw_tables.h), else the uniform one
             uint32_t p = T.dt_plog2;
             if (kPl) p = infw_dt_parts_of(s_pl[(lst - 1) & (INFW_DT_PL_LISTS - 1)], lst - 1, INFW_DT_PL_LISTS, cls, p);
@@ -937,7 +833,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
             result = dt_lookup<kHalf>(T.dte, T.dtl, lst - 1, cls, val, T.dt_plog2, p);
         }
         // ---- first match, one lane per rule, G packets in flight
-        uint64_t pending = (G == 0 || (kAblate & 2)) ? 0 : __ballot(cnt != 0);
+        uint64_t pending = G == 0 ? 0 : __ballot(cnt != 0);
         while (G > 0 && pending) {
             constexpr int GG = G > 0 ? G : 1;
             int j[GG];
@@ -972,7 +868,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         // ---- verdict (kernel.c:444-456) and statistics (kernel.c:376-387)
         const uint32_t action = result & 0xFFu;
         const uint32_t key = (result >> 8) & 0xFFFFu;
-        if (!(kAblate & 4)) {
+        {
             // counter slot of this packet, or -1 (no stats: UNDEF, action outside {1,2}, key >= 1024)
             const int s0_ = (valid && (action == INFW_XDP_DROP || action == INFW_XDP_PASS) && key < kStatKeys)
                                 ? (int)key * 2 + (action == INFW_XDP_DROP) : -1;
@@ -1020,15 +916,14 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
         }
         if (valid) {
             if (results) {
-                if (!(kAblate & 16)) __builtin_nontemporal_store(result, &results[i]);
-                else results[i] = result;
+                __builtin_nontemporal_store(result, &results[i]);
             }
             if (verdicts)
                 verdicts[i] = (pk == INFW_PK_DROP_SHORT || action == INFW_XDP_DROP) ? INFW_XDP_DROP : INFW_XDP_PASS;
 
         }
         // every workgroup runs the same number of tiles, so the barrier is uniform
-        if (!(kAblate & 4) && ++tiles_since_flush == T.stat_flush_tiles) {
+        if (++tiles_since_flush == T.stat_flush_tiles) {
             __syncthreads();
             flush_counters();
             __syncthreads();
@@ -1040,285 +935,268 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     flush_counters();
 }
 
-template <int kBlock, int G, int kAblate = 0, bool kEvents = false, int kWaves = (kBlock == 512 ? 8 : 6),
-          bool kDebug = false, bool kC = false, int kLog = kC24LogDefault, int kB6Log = 0, bool kLean = false,
-          bool kF = false, int kV6 = 2, bool kPl = false, bool kD16 = false, bool kSplit = false, bool kHalf = false>
-void launch(uint32_t grid_per_cu, uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n,
-            uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream,
-            const Sideband &sb = Sideband{}) {
-    const uint64_t tiles = (n + kBlock - 1) / kBlock;
-    const uint64_t grid = (uint64_t)grid_per_cu * cus;
-    const uint32_t g = (uint32_t)(tiles < grid ? tiles : grid);
-    hipLaunchKernelGGL((classify_kernel<kBlock, G, kAblate, kEvents, kWaves, kDebug, kC, kLog, kB6Log, !(kAblate & 128), kLean, kF, kV6, kPl, kD16, kSplit, kHalf>),
-                       dim3(g), dim3(kBlock), 0,
-                       stream, *T, *in, n, results, verdicts, st, sb);
-}
-
-bool d16_big() {
-    static const bool big = [] {
-        const char *e = getenv("INFW_D16_CACHE");
-        return !(e && strcmp(e, "small") == 0);
-    }();
-    return big;
-}
-
-// The decision-table kernel without sidebands: launch shape (block, resident blocks per CU) and
-// LDS word-cache size (1 << log entries) within what each shape's LDS budget allows.  Blocks are
-// multiples of 256 threads: other sizes spread their waves unevenly over the 4 SIMDs (measured
-// 640 x 3, 896 x 2, 448 x 4, 384 x 4: 25-40 % slower than 768 x 2).
-template <bool kC>
-bool launch_shape(int block, uint32_t bpc, int log, bool b6, uint32_t cus, const infw_dev_tables *T, const BatchIn *in,
-                  uint64_t n, uint32_t *results, uint8_t *verdicts, unsigned long long *st, hipStream_t stream) {
-    if (block == 512 && bpc == 4 && log == 10) launch<512, 0, 0, false, 8, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 512 && bpc == 3 && log == 10) launch<512, 0, 0, false, 6, false, kC, 10>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 512 && bpc == 3 && log == 11 && b6) launch<512, 0, 0, false, 6, false, kC, 11, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 512 && bpc == 3 && log == 11) launch<512, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 512 && bpc == 2 && log == 11) launch<512, 0, 0, false, 4, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 11) launch<768, 0, 0, false, 6, false, kC, 11>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    // the default shape: without the rare paths when the epoch has none (lean), per IPv6 group-table form; with
-    // per-list part counts their LDS copy takes half the word cache (INFW_DT_ADAPT=0 at compile: none)
-    // sparse short tables with /16 words (d16_on), with and without per-list part counts
-    // the /16-word cache takes the LDS the shape leaves free — 2048 entries beside the part counts, 4096 without them
-    // and a 256-entry IPv6 group cache (68 / 76 KiB per workgroup): same-box alternating A/B against half of it
-    // (INFW_D16_CACHE=small), configs[1] 1.154 -> 1.108 ms (+4 %), configs[4] even (profiles/r04g)
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on && T->n_dt_pl == INFW_DT_PL_LISTS) {
-        if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else launch<768, 0, 0, false, 6, false, kC, 11, 9, true, false, 0, true, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    } else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->d16_on) {
-        // decision lines read half-first when the compiler chose it (choose_dt_half: configs[1]-like epochs)
-        if (T->dt_half && d16_big())
-            launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else if (d16_big()) launch<768, 0, 0, false, 6, false, kC, 13, 8, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, false, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
+// ---- the registry of instantiations and the selector ------------------------------------------------------------
+// Every classify_kernel instantiation the library launches is one entry of kVariants; select() maps a launch (the
+// epoch's kind, the batch form, the launch shape, the sidebands) onto exactly one key, and a key without an entry
+// is an error, not a fallback.  tests/test_variants*.py enumerate the registry through the C ABI
+// (infw_kernel_variant_name), reach each entry with a table and launch shape built for it and compare it with the
+// oracle.
+struct VKey {
+    uint8_t in;      // INFW_INPUT_*
+    uint16_t block;
+    uint8_t waves, group, log, b6log;
+    bool ev, dbg, lean, pl, d16, split, half;
+    bool operator==(const VKey &o) const {
+        return in == o.in && block == o.block && waves == o.waves && group == o.group && log == o.log &&
+               b6log == o.b6log && ev == o.ev && dbg == o.dbg && lean == o.lean && pl == o.pl && d16 == o.d16 &&
+               split == o.split && half == o.half;
     }
-    // with per-list part counts (16 KiB of LDS) a 4096-entry word cache and a 256-entry IPv6 group cache: same-box
-    // alternating A/B against 2048 + 512 at configs[2], 2.361 vs 2.378 ms (profiles/r03zc)
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean && !T->b2n)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && T->lean)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, true, false, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6 && !T->b2n)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, false, false, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12 && b6)
-        launch<768, 0, 0, false, 6, false, kC, 12, 9, false, false, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else if (block == 768 && bpc == 2 && log == 12) launch<768, 0, 0, false, 6, false, kC, 12>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    else return false;
-    return true;
+};
+
+using RunFn = void (*)(uint32_t grid, const infw_dev_tables &T, const BatchIn &in, uint64_t n, uint32_t *results,
+                       uint8_t *verdicts, unsigned long long *st, hipStream_t stream, const Sideband &sb);
+
+template <int kBlock, int G, int kWaves, int kIn, int kLog, int kB6, bool kEv, bool kDbg, bool kLean, bool kPl,
+          bool kD16, bool kSplit, bool kHalf>
+void run(uint32_t grid, const infw_dev_tables &T, const BatchIn &in, uint64_t n, uint32_t *results, uint8_t *verdicts,
+         unsigned long long *st, hipStream_t stream, const Sideband &sb) {
+    hipLaunchKernelGGL((classify_kernel<kBlock, G, kWaves, kIn, kLog, kB6, kEv, kDbg, kLean, kPl, kD16, kSplit, kHalf>),
+                       dim3(grid), dim3(kBlock), 0, stream, T, in, n, results, verdicts, st, sb);
 }
 
-// Phase 1 of the two-phase form: the default 768 x 2 shape of the epoch's kind, writing split words.
-template <bool kC, bool kLean, bool kPl, bool kD16>
-void launch_phase1(uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n, unsigned long long *st,
-                   hipStream_t stream) {
-    constexpr int kLog = kPl && kD16 ? 11 : 12;
-    launch<768, 0, 0, false, 6, false, kC, kLog, 9, kLean, false, 2, kPl, kD16, true>(2, cus, T, in, n, nullptr, nullptr,
-                                                                                       st, stream);
+struct Variant {
+    VKey key;
+    RunFn fn;
+};
+template <int kBlock, int G, int kWaves, int kIn, int kLog, int kB6, bool kEv, bool kDbg, bool kLean, bool kPl,
+          bool kD16, bool kSplit, bool kHalf>
+constexpr Variant V() {
+    return Variant{VKey{(uint8_t)kIn, (uint16_t)kBlock, (uint8_t)kWaves, (uint8_t)G, (uint8_t)kLog, (uint8_t)kB6, kEv,
+                        kDbg, kLean, kPl, kD16, kSplit, kHalf},
+                   &run<kBlock, G, kWaves, kIn, kLog, kB6, kEv, kDbg, kLean, kPl, kD16, kSplit, kHalf>};
 }
-template <bool kC>
-void launch_phase1_of(uint32_t cus, const infw_dev_tables *T, const BatchIn *in, uint64_t n, unsigned long long *st,
-                      hipStream_t stream) {
-    const bool pl = T->n_dt_pl == INFW_DT_PL_LISTS, d16 = T->d16_on != 0;
-    if (T->lean) {
-        if (pl && d16) launch_phase1<kC, true, true, true>(cus, T, in, n, st, stream);
-        else if (pl) launch_phase1<kC, true, true, false>(cus, T, in, n, st, stream);
-        else if (d16) launch_phase1<kC, true, false, true>(cus, T, in, n, st, stream);
-        else launch_phase1<kC, true, false, false>(cus, T, in, n, st, stream);
+constexpr bool F = false, T_ = true;
+constexpr int S = INFW_INPUT_SOA, C = INFW_INPUT_COMPACT, R = INFW_INPUT_FRAMES;
+
+// LDS per workgroup of the 768-thread shapes: the word cache (8 B x 2^log) and the IPv6 group cache (32 B x 2^b6)
+// take what the counters (2 KiB), the ifindex map (2 KiB), the per-list part counts (16 KiB, pl) and the frame
+// windows (frames) leave of 80 KiB (two workgroups per CU).  Measured choices: 4096 words + 512 groups at configs[2]
+// (profiles/r03zc), 8192 /16 words + 256 groups for /16-word epochs without part counts (profiles/r04g).
+static const Variant kVariants[] = {
+    //   block G  W  in log b6  ev dbg lean pl  d16 split half
+    // the default shape, 768 x 2 (24 waves per CU), per epoch kind
+    V<768, 0, 6, S, 12, 9, F, F, F, F, F, F, F>(),
+    V<768, 0, 6, S, 12, 9, F, F, T_, F, F, F, F>(),
+    V<768, 0, 6, S, 12, 9, F, F, T_, T_, F, F, F>(),
+    V<768, 0, 6, S, 12, 9, F, F, T_, T_, T_, F, F>(),
+    V<768, 0, 6, S, 13, 8, F, F, T_, F, T_, F, F>(),
+    V<768, 0, 6, S, 13, 8, F, F, T_, F, T_, F, T_>(),
+    // phase 1 of the two-phase form (lean epochs with many distinct rule lists; phase 2 is decide_kernel)
+    V<768, 0, 6, S, 12, 9, F, F, T_, F, F, T_, F>(),
+    V<768, 0, 6, S, 12, 9, F, F, T_, T_, F, T_, F>(),
+    V<768, 0, 6, S, 12, 9, F, F, T_, F, T_, T_, F>(),
+    V<768, 0, 6, S, 11, 9, F, F, T_, T_, T_, T_, F>(),
+    // the other decision-table shapes infw_set_launch accepts: any epoch
+    V<512, 0, 4, S, 11, 0, F, F, F, F, F, F, F>(),
+    V<512, 0, 6, S, 11, 8, F, F, F, F, F, F, F>(),
+    V<512, 0, 8, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<256, 0, 6, S, 10, 0, F, F, F, F, F, F, F>(),
+    // the one-lane-per-rule ballot scan (kernel.c:222-258 in rule order), G packets in flight
+    V<512, 1, 8, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<512, 4, 8, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<512, 8, 8, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<256, 1, 6, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<256, 4, 6, S, 10, 0, F, F, F, F, F, F, F>(),
+    V<256, 8, 6, S, 10, 0, F, F, F, F, F, F, F>(),
+    // sidebands (deny events, debug lookup capture): 512 x 3 with them compiled in
+    V<512, 0, 6, S, 10, 0, T_, F, F, F, F, F, F>(),
+    V<512, 0, 6, S, 10, 0, F, T_, F, F, F, F, F>(),
+    V<512, 0, 6, S, 10, 0, T_, T_, F, F, F, F, F>(),
+    // the family-compact layout: the default shape per epoch kind, 512 x 3 for every other shape, debug capture
+    V<768, 0, 6, C, 12, 9, F, F, F, F, F, F, F>(),
+    V<768, 0, 6, C, 12, 9, F, F, T_, F, F, F, F>(),
+    V<768, 0, 6, C, 12, 9, F, F, T_, T_, F, F, F>(),
+    V<768, 0, 6, C, 12, 9, F, F, T_, T_, T_, F, F>(),
+    V<768, 0, 6, C, 13, 8, F, F, T_, F, T_, F, F>(),
+    V<768, 0, 6, C, 13, 8, F, F, T_, F, T_, F, T_>(),
+    V<512, 0, 6, C, 11, 0, F, F, F, F, F, F, F>(),
+    V<512, 0, 6, C, 10, 0, F, T_, F, F, F, F, F>(),
+    // raw frames: 768 x 2, the word cache halved for the frame windows (and again beside the part counts)
+    V<768, 0, 6, R, 11, 9, F, F, F, F, F, F, F>(),
+    V<768, 0, 6, R, 10, 9, F, F, F, T_, F, F, F>(),
+    V<768, 0, 6, R, 11, 9, F, F, T_, F, F, F, F>(),
+    V<768, 0, 6, R, 10, 9, F, F, T_, T_, F, F, F>(),
+    V<768, 0, 6, R, 11, 9, F, F, T_, F, T_, F, F>(),
+    V<768, 0, 6, R, 10, 9, F, F, T_, T_, T_, F, F>(),
+    V<512, 0, 6, R, 10, 0, T_, F, F, F, F, F, F>(),
+    V<512, 0, 6, R, 10, 0, F, T_, F, F, F, F, F>(),
+    V<512, 0, 6, R, 10, 0, T_, T_, F, F, F, F, F>(),
+};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+constexpr int kDecideBlock = 512, kDecideBpc = 2;  // decide_kernel: 2 x 512 per CU (profiles/r04e: 40.3 vs 39.1 Gpps at 4)
+
+void variant_name(const VKey &k, char *buf, size_t cap) {
+    static const char *const in[] = {"soa", "compact", "frames"};
+    snprintf(buf, cap, "%s.%u.w%u.g%u.c%u.b%u%s%s%s%s%s%s%s", in[k.in], k.block, k.waves, k.group, k.log, k.b6log,
+             k.lean ? ".lean" : "", k.pl ? ".pl" : "", k.d16 ? ".d16" : "", k.half ? ".half" : "",
+             k.split ? ".split" : "", k.ev ? ".ev" : "", k.dbg ? ".dbg" : "");
+}
+
+const Variant *find_variant(const VKey &k) {
+    for (const Variant &v : kVariants)
+        if (v.key == k) return &v;
+    return nullptr;
+}
+
+bool dflt_shape(const infw_launch_args &a) { return a.block == 768 && a.blocks_per_cu == 2 && a.group == 0; }
+bool has_sidebands(const infw_launch_args &a) { return a.ev_count != nullptr || a.dbg_fp != nullptr; }
+
+// The one selector.  allow_split = false gives the fused kernel of a two-phase epoch (its scratch could not be had).
+VKey select_variant(const infw_launch_args &a, bool allow_split, uint32_t *bpc) {
+    const infw_dev_tables &T = *a.T;
+    const bool lean = T.lean != 0, pl = T.n_dt_pl == INFW_DT_PL_LISTS, d16 = T.d16_on != 0;
+    VKey k{};
+    k.in = (uint8_t)a.input;
+    if (has_sidebands(a)) {  // 512 x 3 with the sidebands compiled in
+        k.block = 512, k.waves = 6, k.log = 10;
+        k.ev = a.ev_count != nullptr, k.dbg = a.dbg_fp != nullptr;
+        *bpc = 3;
+        return k;
+    }
+    if (a.input == INFW_INPUT_FRAMES) {  // any shape: 768 x 2
+        k.block = 768, k.waves = 6, k.b6log = 9, k.log = pl ? 10 : 11;
+        k.lean = lean, k.pl = pl, k.d16 = lean && d16;
+        *bpc = 2;
+        return k;
+    }
+    if (dflt_shape(a)) {
+        k.block = 768, k.waves = 6, k.b6log = 9, k.log = 12;
+        *bpc = 2;
+        if (!lean) return k;
+        k.lean = true;
+        if (a.input == INFW_INPUT_SOA && T.split && allow_split) {
+            k.split = true, k.pl = pl, k.d16 = d16;
+            if (pl && d16) k.log = 11;
+            return k;
+        }
+        if (d16 && !pl) {  // /16 words without part counts: 8192 /16 words, 256 IPv6 groups
+            k.d16 = true, k.half = T.dt_half != 0, k.log = 13, k.b6log = 8;
+            return k;
+        }
+        k.pl = pl, k.d16 = d16 && pl;
+        return k;
+    }
+    if (a.input == INFW_INPUT_COMPACT) {  // every other shape: 512 x 3
+        k.block = 512, k.waves = 6, k.log = 11;
+        *bpc = 3;
+        return k;
+    }
+    *bpc = (uint32_t)a.blocks_per_cu;
+    k.block = (uint16_t)a.block, k.group = (uint8_t)a.group;
+    if (a.group) {
+        k.waves = a.block == 512 ? 8 : 6, k.log = 10;
+        return k;
+    }
+    if (a.block == 256) k.waves = 6, k.log = 10;
+    else if (a.blocks_per_cu == 2) k.waves = 4, k.log = 11;
+    else if (a.blocks_per_cu == 3) k.waves = 6, k.log = 11, k.b6log = 8;
+    else k.waves = 8, k.log = 10;
+    return k;
+}
+
+BatchIn batch_of(const infw_launch_args &a) {
+    BatchIn bi{};
+    if (a.input == INFW_INPUT_COMPACT) {
+        const infw_batch_soa_c *c = a.compact;
+        bi.saddr4 = c->saddr4, bi.v6tail = c->v6tail, bi.ifindex = c->ifindex, bi.pkt_len = c->pkt_len;
+        bi.meta = c->meta, bi.l4word = c->l4word;
+    } else if (a.input == INFW_INPUT_FRAMES) {
+        const infw_frame_batch *f = a.frames;
+        bi.ifindex = f->ifindex, bi.pkt_len = f->pkt_len, bi.frames = f->frames, bi.offsets = f->offsets;
+        bi.fstride = f->stride, bi.linear_len = f->linear_len;
     } else {
-        if (pl && d16) launch_phase1<kC, false, true, true>(cus, T, in, n, st, stream);
-        else if (pl) launch_phase1<kC, false, true, false>(cus, T, in, n, st, stream);
-        else if (d16) launch_phase1<kC, false, false, true>(cus, T, in, n, st, stream);
-        else launch_phase1<kC, false, false, false>(cus, T, in, n, st, stream);
+        const infw_batch_soa *s = a.soa;
+        bi.saddr = s->saddr, bi.ifindex = s->ifindex, bi.pkt_len = s->pkt_len, bi.meta = s->meta, bi.l4word = s->l4word;
     }
+    return bi;
 }
 
-// The two-phase form (see decide_kernel): the split words live in stream-ordered scratch (hipMallocAsync from the
-// device's default pool, kept mapped between calls), so concurrent classify calls on other streams never share it.
-// Returns 0, -5 on a launch error, or 1 when the scratch cannot be allocated (the caller then runs the fused kernel).
-int launch_split(const infw_dev_tables *T, BatchIn bi, uint64_t n, uint32_t *results, uint8_t *verdicts,
-                 unsigned long long *st, uint32_t cus, hipStream_t stream, bool compact) {
-    static bool pool_kept[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -5;
-    if (dev < 64 && !pool_kept[dev]) {
-        hipMemPool_t pool;
-        uint64_t keep = ~0ull;
-        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess)
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-        pool_kept[dev] = true;
-    }
-    uint64_t *mid = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void **>(&mid), n * sizeof(uint64_t), stream) != hipSuccess) {
-        (void)hipGetLastError();  // no room for the words: the caller runs the fused kernel instead
-        return 1;
-    }
-    bi.mid = mid;
-    if (compact) launch_phase1_of<true>(cus, T, &bi, n, st, stream);
-    else launch_phase1_of<false>(cus, T, &bi, n, st, stream);
-    constexpr int kB = 512;
-    static const uint64_t bpc = [] {  // resident decide workgroups per CU (tuning: INFW_DECIDE_BPC)
-        const char *e = getenv("INFW_DECIDE_BPC");
-        const int v = e ? atoi(e) : 0;
-        return (uint64_t)(v >= 1 && v <= 4 ? v : 2);  // 2: profiles/r04e (40.3 vs 39.1 Gpps at 4)
-    }();
-    const uint64_t tiles = (n + kB - 1) / kB, grid = bpc * cus;
-    hipLaunchKernelGGL(decide_kernel<kB>, dim3((uint32_t)(tiles < grid ? tiles : grid)), dim3(kB), 0, stream, *T,
-                       (const uint64_t *)mid, bi.pkt_len, n, results, verdicts, st);
-    const bool ok = hipGetLastError() == hipSuccess;
-    (void)hipFreeAsync(mid, stream);
-    return ok ? 0 : -5;
+uint32_t grid_of(uint64_t n, int block, uint32_t bpc, uint32_t cus) {
+    const uint64_t tiles = (n + block - 1) / block, grid = (uint64_t)bpc * cus;
+    return (uint32_t)(tiles < grid ? tiles : grid);
 }
 
 }  // namespace
 
-// Host-side launcher (called from abi.cpp).
-//   block: 256 or 512 threads; group: 0 = decision tables (default), else the
-//   one-lane-per-rule ballot scan with that many packets in flight (1, 4, 8);
-//   blocks_per_cu: resident workgroups per CU (LDS: 34 KiB each).
-//   in_c (optional): the family-compact layout instead of `in` (default launch shape).
-extern "C" int infw_launch_classify(const infw_dev_tables *T, const infw_batch_soa *in_s, uint64_t n,
-                                    uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                    int block, int group, int blocks_per_cu, hipStream_t stream,
-                                    infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
-                                    uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count, uint32_t dbg_slots,
-                                    const infw_batch_soa_c *in_c) {
-    if (n == 0) return 0;
-    BatchIn bi{};
-    if (in_c) {
-        bi = BatchIn{nullptr, in_c->saddr4, in_c->v6tail, in_c->ifindex, in_c->pkt_len, in_c->meta, in_c->l4word};
-    } else {
-        bi = BatchIn{in_s->saddr, nullptr, nullptr, in_s->ifindex, in_s->pkt_len, in_s->meta, in_s->l4word};
-    }
-    const BatchIn *in = &bi;
-    uint32_t bpc = (uint32_t)blocks_per_cu;
-    if (ev_count || dbg_fp) {  // sidebands: 512 x 3 (24 waves per CU) with them compiled in
-        bpc = 3;
-        auto *stt = reinterpret_cast<unsigned long long *>(stats);
-        const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
-                          DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
-        if (in_c) {
-            if (ev_count && dbg_fp) launch<512, 0, 0, true, 6, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else if (ev_count) launch<512, 0, 0, true, 6, false, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else launch<512, 0, 0, false, 6, true, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-        } else {
-            if (ev_count && dbg_fp) launch<512, 0, 0, true, 6, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else if (ev_count) launch<512, 0, 0, true, 6, false>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-            else launch<512, 0, 0, false, 6, true>(bpc, cus, T, in, n, results, verdicts, stt, stream, sb);
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -5;
-    }
-    auto *st = reinterpret_cast<unsigned long long *>(stats);
-    // the two-phase form for epochs that chose it (abi.cpp bind_view), in the default launch shape
-    if (T->split && group == 0 && block == 768 && bpc == 2 && !getenv("INFW_ABLATE") && !getenv("INFW_LDS_ABLATE")) {
-        const int rc = launch_split(T, bi, n, results, verdicts, st, cus, stream, in_c != nullptr);
-        if (rc <= 0) return rc;  // 1: scratch allocation failed, fall through to the fused kernel
-    }
-    // LDS attribution (diagnostic, tools/lds_ablate.sh): the default lean shape without one LDS structure each —
-    // 1 the DIR-24-8 word cache, 2 the IPv6 group cache, 4 the LDS counters (no statistics: results stay valid,
-    // counters do not), 7 all three.  SQ_LDS_BANK_CONFLICT of the default minus each variant attributes the rate.
-    if (const char *e = getenv("INFW_LDS_ABLATE")) {
-        if (!in_c && group == 0 && block == 768 && bpc == 2 && T->lean && !T->b2n && T->n_dt_pl == INFW_DT_PL_LISTS) {
-            switch (atoi(e)) {
-            case 1: launch<768, 0, 1024, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-            case 2: launch<768, 0, 0, false, 6, false, false, 11, 0, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-            case 4: launch<768, 0, 4, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-            case 7: launch<768, 0, 4 | 1024, false, 6, false, false, 11, 0, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-            default: launch<768, 0, 0, false, 6, false, false, 11, 9, true, false, 0, true>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-            }
-            return hipGetLastError() == hipSuccess ? 0 : -5;
-        }
-    }
-    const char *env_l = getenv("INFW_C24LOG");  // tuning
-    const int env_log = env_l ? atoi(env_l) : 0;
-    const int log = env_log ? env_log : (block == 768 ? 12 : bpc <= 3 ? 11 : 10);
-    if (group == 0 && !getenv("INFW_ABLATE")) {
-        const char *env_b6 = getenv("INFW_B6CACHE");  // tuning: 0 disables the IPv6 group cache
-        const bool b6 = !env_b6 || atoi(env_b6) != 0;
-        const bool ok = in_c ? launch_shape<true>(block, bpc, log, b6, cus, T, in, n, results, verdicts, st, stream)
-                             : launch_shape<false>(block, bpc, log, b6, cus, T, in, n, results, verdicts, st, stream);
-        if (ok) return hipGetLastError() == hipSuccess ? 0 : -5;
-    }
-    if (in_c) {  // any other shape: the compact layout runs 512 x 3
-        launch<512, 0, 0, false, 6, false, true, 11>(3, cus, T, in, n, results, verdicts, st, stream);
-        return hipGetLastError() == hipSuccess ? 0 : -5;
-    }
-    if (block != 256 && block != 512) {  // shapes without their own instantiation: 512 x 3
-        block = 512;
-        bpc = 3;
-    }
-    if (const char *e = getenv("INFW_ABLATE")) {  // diagnostic builds of the 512/8 shape; results are not valid
-        switch (atoi(e)) {
-        case 0: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 1: launch<512, 0, 1>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 2: launch<512, 0, 2>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 4: launch<512, 0, 4>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 8: launch<512, 0, 8>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 3: launch<512, 0, 3>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 128: launch<512, 0, 128>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 64: launch<512, 0, 64>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 16: launch<512, 0, 16>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 32: launch<512, 0, 32>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 512: launch<512, 0, 512>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        case 17: launch<512, 0, 17>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        default: launch<512, 0, 0>(bpc, cus, T, in, n, results, verdicts, st, stream); break;
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -5;
-    }
-    if (group == 0) {
-        if (block == 256) launch<256, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else if (bpc <= 3) launch<512, 0, 0, false, 6>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else launch<512, 0>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    } else if (block == 256) {
-        if (group == 1) launch<256, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else if (group == 4) launch<256, 4>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else launch<256, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    } else {
-        if (group == 1) launch<512, 1>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else if (group == 4) launch<512, 4>(bpc, cus, T, in, n, results, verdicts, st, stream);
-        else launch<512, 8>(bpc, cus, T, in, n, results, verdicts, st, stream);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+extern "C" int infw_launch_shape_ok(int block, int group, int bpc) {
+    if (group == 0)
+        return (block == 768 && bpc == 2) || (block == 512 && bpc >= 2 && bpc <= 4) || (block == 256 && bpc == 6);
+    return (group == 1 || group == 4 || group == 8) && ((block == 512 && bpc == 3) || (block == 256 && bpc == 6));
 }
 
-// Classification straight from raw frames in HBM (infw_frame_batch; the packer's tuple is built in the kernel,
-// no SoA batch is written or read): 768 x 2 with a 2048-entry word cache, the LDS the frame windows need.
-// Sidebands (deny events, debug lookup capture) run 512 x 3 with them compiled in, like infw_launch_classify's.
-extern "C" int infw_launch_classify_frames(const infw_dev_tables *T, const infw_frame_batch *fb, uint64_t n,
-                                           uint32_t *results, uint8_t *verdicts, uint64_t *stats, uint32_t cus,
-                                           hipStream_t stream, infw_event_rec *ev, uint64_t ev_cap, uint64_t *ev_count,
-                                           uint64_t *dbg_fp, uint32_t *dbg_keys, uint32_t *dbg_count,
-                                           uint32_t dbg_slots) {
-    if (n == 0) return 0;
-    BatchIn bi{};
-    bi.ifindex = fb->ifindex;
-    bi.pkt_len = fb->pkt_len;
-    bi.frames = fb->frames;
-    bi.offsets = fb->offsets;
-    bi.fstride = fb->stride;
-    bi.linear_len = fb->linear_len;
-    auto *st = reinterpret_cast<unsigned long long *>(stats);
-    if (ev_count || dbg_fp) {
-        const Sideband sb{EventSink{ev, ev_cap, reinterpret_cast<unsigned long long *>(ev_count)},
-                          DebugSink{reinterpret_cast<unsigned long long *>(dbg_fp), dbg_keys, dbg_count, dbg_slots - 1}};
-        if (ev_count && dbg_fp)
-            launch<512, 0, 0, true, 6, true, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
-        else if (ev_count)
-            launch<512, 0, 0, true, 6, false, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
-        else
-            launch<512, 0, 0, false, 6, true, false, 10, 0, false, true>(3, cus, T, &bi, n, results, verdicts, st, stream, sb);
-        return hipGetLastError() == hipSuccess ? 0 : -5;
+extern "C" int infw_launch_variant_count(void) { return kNumVariants + 1; }
+
+extern "C" const char *infw_launch_variant_name(int i) {
+    static char names[kNumVariants + 1][96];
+    static const bool init = [] {
+        for (int j = 0; j < kNumVariants; j++) variant_name(kVariants[j].key, names[j], sizeof names[j]);
+        snprintf(names[kNumVariants], sizeof names[kNumVariants], "decide.%d", kDecideBlock);
+        return true;
+    }();
+    (void)init;
+    return i >= 0 && i <= kNumVariants ? names[i] : nullptr;
+}
+
+extern "C" int infw_launch_variant(const infw_launch_args *a, char *name, size_t cap) {
+    uint32_t bpc = 0;
+    const VKey k = select_variant(*a, true, &bpc);
+    char buf[128];
+    variant_name(k, buf, sizeof buf);
+    if (!find_variant(k)) snprintf(buf + strlen(buf), sizeof buf - strlen(buf), "(unregistered)");
+    else if (k.split) snprintf(buf + strlen(buf), sizeof buf - strlen(buf), "+decide.%d", kDecideBlock);
+    if (strlen(buf) + 1 > cap) return -ERANGE;
+    memcpy(name, buf, strlen(buf) + 1);
+    return 0;
+}
+
+// The two-phase form (see decide_kernel): the per-packet words live in stream-ordered scratch from the context's
+// own pool (abi.cpp; trimmed before a full commit uploads), so concurrent classify calls on other streams never share
+// it and no other allocator of the process is affected.  Returns 0, -EIO on a launch error, or 1 when the scratch
+// cannot be allocated (the caller then runs the fused kernel).
+static int launch_split(const infw_launch_args &a, const Variant &p1, BatchIn bi, unsigned long long *st) {
+    uint64_t *mid = nullptr;
+    if (!a.pool || hipMallocFromPoolAsync(reinterpret_cast<void **>(&mid), a.n * sizeof(uint64_t), a.pool, a.stream) !=
+                       hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
     }
-    // with per-list part counts their LDS copy replaces another half of the word cache (2 x 80 KiB per CU)
-    if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean && T->d16_on)  // /16 words (sparse short tables)
-        launch<768, 0, 0, false, 6, false, false, 10, 9, true, true, 2, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    else if (T->lean && T->d16_on && T->n_dt_pl != INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, false, 11, 9, true, true, 2, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    else if (T->n_dt_pl == INFW_DT_PL_LISTS && T->lean)
-        launch<768, 0, 0, false, 6, false, false, 10, 9, true, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    else if (T->n_dt_pl == INFW_DT_PL_LISTS)
-        launch<768, 0, 0, false, 6, false, false, 10, 9, false, true, 2, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    else if (T->lean) launch<768, 0, 0, false, 6, false, false, 11, 9, true, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    else launch<768, 0, 0, false, 6, false, false, 11, 9, false, true>(2, cus, T, &bi, n, results, verdicts, st, stream);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    bi.mid = mid;
+    p1.fn(grid_of(a.n, p1.key.block, 2, a.cus), *a.T, bi, a.n, nullptr, nullptr, st, a.stream, Sideband{});
+    hipLaunchKernelGGL(decide_kernel<kDecideBlock>, dim3(grid_of(a.n, kDecideBlock, kDecideBpc, a.cus)),
+                       dim3(kDecideBlock), 0, a.stream, *a.T, (const uint64_t *)mid, bi.pkt_len, a.n, a.results,
+                       a.verdicts, st);
+    const bool ok = hipGetLastError() == hipSuccess;
+    (void)hipFreeAsync(mid, a.stream);
+    return ok ? 0 : -EIO;
+}
+
+extern "C" int infw_launch_classify(const infw_launch_args *a) {
+    if (a->n == 0) return 0;
+    const BatchIn bi = batch_of(*a);
+    auto *st = reinterpret_cast<unsigned long long *>(a->stats);
+    const Sideband sb{EventSink{a->ev, a->ev_cap, reinterpret_cast<unsigned long long *>(a->ev_count)},
+                      DebugSink{reinterpret_cast<unsigned long long *>(a->dbg_fp), a->dbg_keys, a->dbg_count,
+                                a->dbg_slots ? a->dbg_slots - 1 : 0u}};
+    uint32_t bpc = 0;
+    VKey k = select_variant(*a, true, &bpc);
+    const Variant *v = find_variant(k);
+    if (v && k.split) {
+        const int rc = launch_split(*a, *v, bi, st);
+        if (rc <= 0) return rc;
+        k = select_variant(*a, false, &bpc);  // no scratch: the fused kernel
+        v = find_variant(k);
+    }
+    if (!v) return -EIO;  // a selector result without a registry entry (tests/test_variants_cpu.py rules it out)
+    v->fn(grid_of(a->n, k.block, bpc, a->cus), *a->T, bi, a->n, a->results, a->verdicts, st, a->stream, sb);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -156,13 +156,11 @@ void tables_io(IO &io, M &h) {  // HostTables fields, in one order for both dire
     io.pod(h.n_tbl8_groups);
     io.vec(h.tbl24);
     io.vec(h.tbl8);
-    io.pod(h.d24_inline);
     io.pod(h.short_mode);
     io.vec(h.ltab);
     io.vec(h.btab);
     io.pod(h.n_buckets);
     io.pod(h.n_overflow_groups);
-    io.pod(h.b2n);
     io.vec(h.wild);
     io.pod(h.n_wild);
     io.vec(h.levels);
@@ -172,8 +170,6 @@ void tables_io(IO &io, M &h) {  // HostTables fields, in one order for both dire
     io.vec(h.dtl);
     io.pod(h.dt_plog2);
     io.vec(h.dt_pl);
-    io.vec(h.dxr_idx);
-    io.vec(h.dxr_lines);
     io.vec(h.d16);
     io.pod(h.d16_on);
     io.pod(h.d16_permille);
@@ -253,8 +249,8 @@ bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std
     const uint64_t per_list = (uint64_t)INFW_NCLS << h.dt_plog2;
     // never-empty device buffers (the compiler keeps a placeholder element in each)
     if (h.tbl24.empty() || h.tbl8.empty() || h.nodes.empty() || h.vpool.empty() || h.rules.empty() ||
-        h.dtl.empty() || h.dte.empty() || h.desc.empty() || h.wild.size() < 3 || h.dxr_idx.empty() ||
-        h.dxr_lines.empty() || h.d16.empty() || h.l16.empty())
+        h.dtl.empty() || h.dte.empty() || h.desc.empty() || h.wild.size() < 3 || h.d16.empty() ||
+        h.l16.empty())
         return bad("empty table buffer");
     // ifindex map
     const uint64_t nif = h.if_keys.size();
@@ -300,8 +296,8 @@ bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std
         if (w & INFW_D24_ABA) return (w & INFW_D24_ABA_MAXV) <= L && ((w >> 22) & INFW_D24_ABA_MAXV) <= L;
         return (w & INFW_D24_MAXV) <= L && ((w >> 15) & INFW_D24_MAXV) <= L && ((w >> 30) & INFW_D24_MAXV) <= L;
     };
-    const bool dir24_image = h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_DXR;
-    if (h.short_mode > INFW_SHORT_DXR) return bad("short-table form");
+    const bool dir24_image = h.short_mode == INFW_SHORT_DIR24;
+    if (h.short_mode > INFW_SHORT_NONE) return bad("short-table form");
     if (dir24_image) {
         if (h.n_slots == 0 || h.tbl24.size() != ((uint64_t)h.n_slots << 24)) return bad("DIR-24-8 size");
         if (h.tbl8.size() % 256 || h.tbl8.size() < h.n_tbl8_groups * 256) return bad("tbl8 size");
@@ -316,14 +312,6 @@ bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std
         if (h.short_mode != INFW_SHORT_DIR24 || h.d16.size() != ((uint64_t)h.n_slots << 16)) return bad("/16 words");
         for (uint64_t w : h.d16)
             if ((w & INFW_D16_INLINE) && ((w & 0x7FFFu) > L || ((w >> 15) & 0x7FFFu) > L)) return bad("/16 word value");
-    }
-    if (h.short_mode == INFW_SHORT_DXR) {
-        if (h.dxr_idx.size() != ((uint64_t)h.n_slots << 16)) return bad("range index size");
-        for (uint32_t w : h.dxr_idx)
-            if ((w & INFW_DXR_DIRECT) ? (w & ~INFW_DXR_DIRECT) > L : w >= h.dxr_lines.size()) return bad("range index word");
-        for (const infw_dt_line &l : h.dxr_lines)
-            for (uint32_t j = 5; j < 16; j++)
-                if (l.w[j] > L) return bad("range line value");
     }
     if (h.short_mode == INFW_SHORT_COMPRESSED) {
         if (h.l16.size() != ((uint64_t)std::max<uint32_t>(h.n_slots, 1) << 16)) return bad("compressed short-table size");
@@ -371,18 +359,7 @@ bool check_tables(const HostTables &h, const IncState &inc, uint64_t n_vals, std
     if (!l_free) return bad("long table without a free entry");
     auto rec_ok = [&](const infw_v6_rec &r) { return (r.meta & 0x1FFFFFFu) <= L && (r.meta >> 25) >= 1 && (r.meta >> 25) <= 96; };
     uint64_t overflowed = 0;
-    if (h.b2n) {
-        if (h.btab.size() != h.b2n) return bad("IPv6 slot-form size");
-        const infw_v6_slot *s = reinterpret_cast<const infw_v6_slot *>(h.btab.data());
-        for (uint64_t i = 0; i < 2 * h.b2n; i++) {
-            if (!s[i].tag) continue;
-            const uint32_t nr = s[i].info & 0xFFu;
-            if (s[i].tag > h.n_slots || (nr != 1 && nr != 2 && nr != INFW_BUCKET_OVERFLOW) ||
-                (nr != INFW_BUCKET_OVERFLOW && !rec_ok(s[i].rec)))
-                return bad("IPv6 slot");
-            overflowed += nr == INFW_BUCKET_OVERFLOW;
-        }
-    } else {
+    {
         if (!pow2(h.btab.size())) return bad("IPv6 bucket-table size");
         bool b_free = false;
         for (const infw_v6_bucket &b : h.btab) {
@@ -477,36 +454,55 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
         *why = r.ok ? "trailing bytes after the image" : "truncated image";
         return -EINVAL;
     }
-    return check_tables(h, inc, nv, why) ? 0 : -EINVAL;
+    if (!check_tables(h, inc, nv, why)) return -EINVAL;
+    h.dt_short_lines = count_dt_short_lines(h);
+    return 0;
 }
 
 // The committed set as the importer's pending map: values interned in id order (distinct values, so each gets the
 // id it had), then the nodes with their ids, indexed as update() would.  A context whose entries were all removed
 // and committed counts as empty: its leftover value pool and tombstones are dropped first.
+// Everything that can refuse an entry set is checked before the map is touched: a refused import leaves the map (and
+// its value pool, which the committed image's incremental state refers to by value id) exactly as it was.
+static bool entries_distinct(const ImageEntries &ent, std::string *why) {
+    const uint64_t nv = ent.vals.size() / 1200;
+    std::vector<std::pair<uint64_t, uint64_t>> hv(nv);  // (hash, index)
+    for (uint64_t i = 0; i < nv; i++) hv[i] = {xxh64(ent.vals.data() + 1200 * i, 1200), i};
+    std::sort(hv.begin(), hv.end());
+    for (uint64_t i = 1; i < nv; i++)
+        if (hv[i].first == hv[i - 1].first &&
+            memcmp(ent.vals.data() + 1200 * hv[i].second, ent.vals.data() + 1200 * hv[i - 1].second, 1200) == 0) {
+            *why = "duplicate values in the image";
+            return false;
+        }
+    std::vector<std::pair<uint64_t, uint64_t>> hk(ent.nodes.size());
+    for (size_t i = 0; i < ent.nodes.size(); i++) hk[i] = {NodeTable::hash(ent.nodes[i].first), i};
+    std::sort(hk.begin(), hk.end());
+    for (size_t i = 1; i < hk.size(); i++)
+        if (hk[i].first == hk[i - 1].first && ent.nodes[hk[i].second].first == ent.nodes[hk[i - 1].second].first) {
+            *why = "duplicate key in the image";
+            return false;
+        }
+    return true;
+}
+
 int PendingMap::install_committed(const ImageEntries &ent, std::string *why) {
     if (!nodes.empty() || !dirty_ids.empty()) {
         *why = "the context already holds entries or uncommitted edits";
         return -EBUSY;
     }
-    clear();
     if (ent.nodes.size() > max_entries) {
         *why = "more entries than max_entries";
         return -ENOSPC;
     }
+    if (!entries_distinct(ent, why)) return -EINVAL;
+    clear();  // an emptied context: its leftover value pool and tombstones go (nothing below refuses)
     const uint64_t nv = ent.vals.size() / 1200;
-    for (uint64_t i = 0; i < nv; i++)
-        if (pool.intern(ent.vals.data() + 1200 * i) != i) {
-            *why = "duplicate values in the image";
-            return -EINVAL;
-        }
+    for (uint64_t i = 0; i < nv; i++) (void)pool.intern(ent.vals.data() + 1200 * i);
     nodes.reserve(ent.nodes.size());
     order_vec.reserve(ent.nodes.size());
     for (const auto &e : ent.nodes) {
         const uint64_t h = NodeTable::hash(e.first);
-        if (nodes.find(e.first, h)) {
-            *why = "duplicate key in the image";
-            return -EINVAL;
-        }
         MapNode *n = nodes.insert(e.first, h);
         n->val = e.second;
         nodes.set_live(n, true);

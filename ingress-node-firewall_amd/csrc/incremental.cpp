@@ -131,7 +131,7 @@ void patch_prepare(const HostTables &h, IncState &inc) {
 }
 
 int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
-                 std::string *why) {
+                 std::string *why, const Options &opt) {
     auto full = [&](const char *reason) {
         if (why) *why = reason;
         return 1;
@@ -183,7 +183,6 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         uint64_t bucket;  // btab index (found or insert position)
         bool found;
         SmallRecs recs;
-        uint32_t b2k = 0, b2n = 0;  // two-choice slot form: first slot and record count of the group
     };
     std::unordered_map<uint64_t, Group> groups;
     groups.reserve(edits.size());
@@ -194,32 +193,14 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     for (const Edit &e : edits) {
         if (e.P <= 32 || h.levels.empty()) continue;
         const uint64_t hh = infw_bucket_hash(e.slot, e.a32);
-        __builtin_prefetch(h.b2n ? &h.btab[INFW_B2_INDEX(hh >> 32, h.b2n)] : &h.btab[hh & bmask]);
+        __builtin_prefetch(&h.btab[hh & bmask]);
     }
     for (const Edit &e : edits) {
         if (e.P <= 32) continue;
         if (h.levels.empty()) return full("first long prefix");
         const uint64_t gk = (uint64_t)e.slot << 32 | e.a32;
         auto git = groups.find(gk);
-        if (git == groups.end() && h.b2n) {  // two-choice slot form: records rewritten in place only
-            Group g;
-            g.found = false;
-            const uint64_t hh = infw_bucket_hash(e.slot, e.a32);
-            const infw_v6_slot *st = reinterpret_cast<const infw_v6_slot *>(h.btab.data());
-            for (uint64_t i : {INFW_B2_INDEX(hh >> 32, h.b2n), INFW_B2_INDEX(hh, h.b2n)}) {
-                for (uint32_t k = 0; k < 2 && !g.found; k++)
-                    if (st[2 * i + k].tag == e.slot + 1 && st[2 * i + k].top == e.a32) {
-                        g.found = true;
-                        g.bucket = i;
-                        g.b2k = k;
-                        g.b2n = st[2 * i + k].info & 0xFFu;
-                    }
-                if (g.found || !(st[2 * i].info & INFW_B2_DISPLACED)) break;
-            }
-            if (g.found && g.b2n == INFW_BUCKET_OVERFLOW) return full("edit in an overflowed IPv6 group");
-            for (uint32_t k = 0; k < g.b2n; k++) g.recs.push_back(st[2 * g.bucket + g.b2k + k].rec);
-            git = groups.emplace(gk, std::move(g)).first;
-        } else if (git == groups.end()) {
+        if (git == groups.end()) {
             Group g;
             uint64_t i = infw_bucket_hash(e.slot, e.a32) & bmask;
             for (;;) {
@@ -253,80 +234,8 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         if (e.now) rv.push_back(infw_v6_rec{e.lo, mid, (e.P - 32) << 25});  // list filled in pass 2
         if (rv.size() > INFW_BUCKET_INLINE) return full("IPv6 group exceeds 3 prefixes");
     }
-    // two-choice slot form: a group keeps its record count in place, a removed group frees its slots (slot 1
-    // moves down so that slot 0 stays in use), a new group of <= 2 records takes free slots in its first
-    // bucket or, marking the first DISPLACED, in its second; anything else recompiles.  Planned on copies of
-    // the buckets involved (`plan`), written back in pass 2.
-    std::unordered_map<uint64_t, std::array<infw_v6_slot, 2>> plan;
-    int64_t b2_delta = 0;  // groups added - removed
-    if (h.b2n) {
-        const infw_v6_slot *st = reinterpret_cast<const infw_v6_slot *>(h.btab.data());
-        auto bucket = [&](uint64_t i) -> std::array<infw_v6_slot, 2> & {
-            auto it = plan.find(i);
-            if (it == plan.end()) {
-                std::array<infw_v6_slot, 2> a;
-                memcpy(a.data(), &st[2 * i], sizeof(a));
-                it = plan.emplace(i, a).first;
-            }
-            return it->second;
-        };
-        std::unordered_map<uint64_t, Group *> at_slot;  // bucket * 2 + slot -> edited group living there
-        for (auto &kv : groups)
-            if (kv.second.found) at_slot[kv.second.bucket * 2 + kv.second.b2k] = &kv.second;
-        for (auto &kv : groups) {  // removals first: they free slots
-            Group &g = kv.second;
-            if (g.recs.size() > 2) return full("IPv6 group exceeds 2 prefixes in the two-choice slot form");
-            if (!g.found || g.recs.size() == g.b2n) continue;
-            if (!g.recs.empty()) return full("IPv6 group size change in the two-choice slot form");
-            auto &b = bucket(g.bucket);
-            const uint32_t flag = b[0].info & INFW_B2_DISPLACED;
-            if (g.b2n == 2 || g.b2k == 1) b[g.b2k == 1 ? 1 : 0] = infw_v6_slot{};
-            if (g.b2n == 2) b[1] = infw_v6_slot{};
-            if (g.b2n == 1 && g.b2k == 0) {
-                b[0] = b[1];
-                b[1] = infw_v6_slot{};
-            }
-            b[0].info = (b[0].info & ~INFW_B2_DISPLACED) | flag;
-            if (g.b2n == 1 && g.b2k == 0) {  // the group that moved from slot 1 to slot 0, if it is edited too
-                auto it = at_slot.find(g.bucket * 2 + 1);
-                if (it != at_slot.end()) {
-                    it->second->b2k = 0;
-                    at_slot[g.bucket * 2] = it->second;
-                    at_slot.erase(it);
-                }
-            }
-            g.found = false;
-            b2_delta--;
-        }
-        for (auto &kv : groups) {  // then new groups
-            Group &g = kv.second;
-            if (g.found || g.recs.empty()) continue;
-            const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
-            const uint64_t hh = infw_bucket_hash(slot, top);
-            const uint64_t i1 = INFW_B2_INDEX(hh >> 32, h.b2n), i2 = INFW_B2_INDEX(hh, h.b2n);
-            const uint32_t need = (uint32_t)g.recs.size();
-            for (uint64_t i : {i1, i2}) {
-                auto &b = bucket(i);
-                const uint32_t k = b[0].tag == 0 ? 0 : b[1].tag == 0 ? 1 : 2;
-                if (k + need > 2) continue;
-                for (uint32_t j = 0; j < need; j++) {
-                    b[k + j].tag = slot + 1;
-                    b[k + j].top = top;
-                    b[k + j].info = (b[k + j].info & INFW_B2_DISPLACED) | need;
-                }
-                if (i != i1) bucket(i1)[0].info |= INFW_B2_DISPLACED;
-                g.found = true;
-                g.bucket = i;
-                g.b2k = k;
-                g.b2n = need;
-                b2_delta++;
-                break;
-            }
-            if (!g.found) return full("no free slot for a new IPv6 group in the two-choice slot form");
-        }
-    }
     // compiled at load <= 1/8; past 1/4 the probe chains a wave waits for grow: recompile
-    if (!h.b2n && (h.n_buckets + new_buckets) * 4 > h.btab.size()) return full("IPv6 bucket table past 1/4 load");
+    if ((h.n_buckets + new_buckets) * 4 > h.btab.size()) return full("IPv6 bucket table past 1/4 load");
     // two new groups may share an insert position: they must not
     {
         std::vector<uint64_t> pos;
@@ -416,7 +325,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
     };
     auto list1 = [&](const NodeVal *v) { return list1_in(memo, v); };
 
-    // IPv6 buckets.  Touches only btab, n_buckets, the groups and their plan (the short-table phase below only
+    // IPv6 buckets.  Touches only btab, n_buckets and the groups (the short-table phase below only
     // the DIR-24-8 words, tbl8 groups and g8bits; both read the map), so with enough of both kinds of edits it
     // runs on a second thread beside the short-table phase.
     std::vector<uint32_t> ifx_of_slot(h.n_slots, 0);
@@ -464,13 +373,6 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
             if (!g.found && g.recs.empty()) continue;
             const uint32_t slot = (uint32_t)(kv.first >> 32), top = (uint32_t)kv.first;
             std::sort(g.recs.begin(), g.recs.end(), [](const infw_v6_rec &a, const infw_v6_rec &c) { return a.meta > c.meta; });
-            if (h.b2n) {  // the planned slots, longest record first
-                auto &b = plan.count(g.bucket) ? plan[g.bucket] : *reinterpret_cast<std::array<infw_v6_slot, 2> *>(
-                                                                       h.btab.data() + g.bucket);
-                for (size_t k = 0; k < g.recs.size(); k++) b[g.b2k + k].rec = g.recs[k];
-                mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
-                continue;
-            }
             infw_v6_bucket &b = h.btab[g.bucket];
             if (!g.found) {
                 b.tag = slot + 1;
@@ -481,10 +383,6 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
             memset(b.rec, 0, sizeof(b.rec));
             for (size_t k = 0; k < g.recs.size(); k++) b.rec[k] = g.recs[k];
             mark(ranges, TB_BTAB, g.bucket * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
-        }
-        for (const auto &kv : plan) {  // two-choice slot form: the planned buckets
-            memcpy(h.btab.data() + kv.first, kv.second.data(), sizeof(infw_v6_bucket));
-            mark(ranges, TB_BTAB, kv.first * sizeof(infw_v6_bucket), sizeof(infw_v6_bucket));
         }
     };
 
@@ -532,7 +430,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                 auto g = h.tbl8_of.find(gkey | i);
                 if (g != h.tbl8_of.end()) {
                     refill_group(ifx, i, g->second, 0, 24, ans[k]);
-                    t24[i] = infw_d24_encode(&h.tbl8[(size_t)g->second << 8], g->second, h.d24_inline);
+                    t24[i] = infw_d24_encode(&h.tbl8[(size_t)g->second << 8], g->second);
                 } else {
                     t24[i] = list1(ans[k]);
                 }
@@ -555,7 +453,7 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
                 h.n_tbl8_groups++;
             }
             refill_group(ifx, i, g, a & 0xFFu, e->P, atP);
-            t24[i] = infw_d24_encode(&h.tbl8[(size_t)g << 8], g, h.d24_inline);
+            t24[i] = infw_d24_encode(&h.tbl8[(size_t)g << 8], g);
             mark(ranges, TB_TBL24, (((uint64_t)e->slot << 24) + i) * 8, 8);
         }
     }
@@ -586,9 +484,16 @@ int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<
         v6_phase();
     }
     ranges.insert(ranges.end(), ranges6.begin(), ranges6.end());
-    h.n_buckets = (uint64_t)((int64_t)h.n_buckets + b2_delta);
     h.n_entries = m.nodes.size();
-    if (getenv("INFW_PATCH_TRACE")) {
+    // half-first decision-line reads: the per-epoch choice follows the lines appended (choose_dt_half's rule over
+    // the running count), so an epoch grown by incremental commits reads its lines the way a compile would choose
+    if (h.n_lists != n_lists_before) {
+        const size_t per_list = (size_t)INFW_NCLS << h.dt_plog2;
+        for (size_t e = (size_t)n_lists_before * per_list; e < (size_t)h.n_lists * per_list && e < h.dte.size(); e++)
+            h.dt_short_lines += infw_dt_line_short(h.dte[e]);
+        h.dt_half = choose_dt_half(h, opt.dt_half);
+    }
+    if (opt.trace & 2) {
         uint32_t minP = 99;
         for (const Edit *e : shorts) minP = std::min(minP, e->P);
         const auto tp3 = std::chrono::steady_clock::now();

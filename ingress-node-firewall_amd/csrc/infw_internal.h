@@ -207,12 +207,10 @@ struct HostTables {
     std::vector<uint64_t> tbl24;        // DIR-24-8 form (short_mode == INFW_SHORT_DIR24), INFW_D24_* words
     std::vector<uint32_t> tbl8;         // 256-value groups of every /24 with entries longer than /24
     std::unordered_map<uint64_t, uint32_t> tbl8_of;  // slot << 24 | /24 -> its group (inline words too)
-    bool d24_inline = true;             // INFW_D24_INLINE=0: every group stays in tbl8 (A/B)
     uint32_t short_mode = INFW_SHORT_DIR24;
     std::vector<infw_long_entry> ltab;
     std::vector<infw_v6_bucket> btab;
     uint64_t n_buckets = 0, n_overflow_groups = 0;
-    uint64_t b2n = 0;                   // != 0: btab in the two-choice slot form (infw_tables.h) with b2n buckets
     std::vector<uint32_t> wild{0u, 0u, 0u};  // prefixLen < 32 entries: {plen, key bits, list+1}, longest first
     uint32_t n_wild = 0;
     std::vector<uint8_t> levels;
@@ -221,17 +219,48 @@ struct HostTables {
     std::vector<infw_dt_line> dte, dtl;  // decision-table entry and leaf lines
     uint32_t dt_plog2 = 0;               // value-axis parts per (list, class): 1 << dt_plog2
     std::vector<uint32_t> dt_pl;         // per-list part counts (INFW_DT_PL_LISTS words) or empty (infw_tables.h)
-    std::vector<uint32_t> dxr_idx;       // short_mode INFW_SHORT_DXR: index words (infw_tables.h)
-    std::vector<infw_dt_line> dxr_lines; //   and range lines
     std::vector<uint64_t> d16;           // d16_on: n_slots << 16 /16 words in front of DIR-24-8 (infw_tables.h)
     uint32_t d16_on = 0;
     uint32_t d16_permille = 0;           // of the /16s holding a prefix longer than /16, those with an inline word
     uint32_t dt_half = 0;                // the kernel reads decision lines half-first (choose_dt_half)
+    uint64_t dt_short_lines = 0;         // entry lines a first half answers (infw_dt_line_short; not serialised)
     uint32_t n_lists = 0;
     uint64_t n_entries = 0;
     uint64_t n_long_entries = 0;
     // A host view with the same walk functions as the device (self-test only).
     infw_dev_tables view() const;
+};
+
+// The device-resident buffers of one image, in upload order.
+enum TableBuf {
+    TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
+    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_D16, TB_COUNT
+};
+// The kernel's view of image h whose buffer b lives at buf[b] (device buffers, or the host vectors for view()).
+infw_dev_tables view_of(const HostTables &h, void *const buf[TB_COUNT]);
+
+// Per-context options (infw_set_option, include/infw.h).  Each one selects among bit-exact forms of the same epoch,
+// the host threads of a compile, how often the kernel flushes its counters, or tracing: none changes a result word,
+// a verdict or a counter.  Defaults are the measured choices; -1 means "chosen per epoch".
+struct Options {
+    int32_t short_table = -1;       // full compiles: -1 DIR-24-8 while n_slots x 128 MiB <= 4 GiB, else compressed;
+                                    // 0 DIR-24-8, 1 the compressed 16-8-8 form
+    int32_t d16 = -1;               // /16 words in front of DIR-24-8: -1 per epoch (build_d16), 0 never, 1 always
+    int32_t dt_half = -1;           // half-first decision-line reads: -1 per epoch (choose_dt_half), 0, 1
+    int32_t dt_parts = 0;           // value parts per (list, class): 0 per epoch (choose_dt_plog2), else 1|2|4|8|16
+    int32_t dt_adapt = 1;           // per-list part counts (<= INFW_DT_PL_LISTS lists): 1 on, 0 off
+    int64_t dt_budget_mb = 2048;    // the entry lines of one image stay below this (fewer parts)
+    int32_t compile_threads = 0;    // host threads of a full compile: 0 = hardware threads (<= 16)
+    int32_t split = -1;             // two-phase classify: -1 when the entry lines exceed split_min_mb, 0 never, 1 always
+    int64_t split_min_mb = 1024;
+    int32_t stat_flush_tiles = 1024; // a workgroup flushes its LDS counters every this many tiles (1..1024)
+    int32_t trace = 0;              // stderr: 1 compile phases, 2 incremental patch phases, 4 commit timing
+};
+// Name, bounds and field of every option (abi.cpp infw_set_option / infw_get_option / infw_option_name).
+struct OptionDef {
+    const char *name;
+    int64_t lo, hi;
+    const char *doc;
 };
 
 // Bookkeeping of the compiled image that an incremental commit patches
@@ -254,20 +283,18 @@ struct IncState {
 // The /16 word of (slot, address bits 0..15) from the DIR-24-8 image: inline when its runs fit, else 0.
 // *runs: 1 for a /16 of one answer throughout (either way).
 uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs = nullptr);
-// Decide whether the epoch gets /16 words (INFW_D16=0/1 forces) and build them; n_short_wide of the n_short
+// Decide whether the epoch gets /16 words (req: Options::d16) and build them; n_short_wide of the n_short
 // <= /32 prefixes are /20 or shorter.
-void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide);
-uint32_t choose_dt_half(const HostTables &h);
+void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide, int req = -1);
+// An entry line whose first 32 B answer every value: a compact leaf of <= 9 segments.
+inline uint32_t infw_dt_line_short(const infw_dt_line &l) {
+    return (l.w[0] & INFW_DT_COMPACT) && !(l.w[0] & INFW_DT_ROOT) && (l.w[0] & 0xFFu) <= 9;
+}
+uint64_t count_dt_short_lines(const HostTables &h);
+// Half-first decision-line reads for this image (req: Options::dt_half), from h.dt_short_lines.
+uint32_t choose_dt_half(const HostTables &h, int req = -1);
 
-// short_mode_req: -1 = automatic (DIR-24-8 while n_slots * 64 MiB <= dir24_budget)
-int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req = -1,
-                   uint64_t dir24_budget = 4ull << 30, IncState *inc = nullptr);
-
-// The device-resident buffers of one image, in upload order.
-enum TableBuf {
-    TB_IFK, TB_IFS, TB_L16, TB_NODES, TB_VPOOL, TB_TBL24, TB_TBL8, TB_LTAB, TB_BTAB,
-    TB_DESC, TB_RULES, TB_DTE, TB_DTL, TB_LEVELS, TB_WILD, TB_DTPL, TB_DXRI, TB_DXRL, TB_D16, TB_COUNT
-};
+int compile_tables(const PendingMap &m, HostTables &out, const Options &opt = Options(), IncState *inc = nullptr);
 // Host bytes of buffer b (at least one element, like the upload).
 void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes);
 struct DirtyRange {
@@ -285,7 +312,7 @@ int image_read(const uint8_t *buf, uint64_t size, const char *build_id, ImageEnt
 // Returns 0 when patched, 1 when the edit needs a full compile (*why says why;
 // nothing was modified), < 0 on error.
 int patch_tables(const PendingMap &m, HostTables &h, IncState &inc, std::vector<DirtyRange> &ranges,
-                 std::string *why);
+                 std::string *why, const Options &opt = Options());
 // The patch's derived indexes (g8bits, lid_of_vid) of a freshly compiled or imported image, built up front so the
 // first incremental commit after it does not pay for them (~5 ms at configs[2]).
 void patch_prepare(const HostTables &h, IncState &inc);

@@ -77,26 +77,6 @@ struct infw_v6_bucket {     // 64 B
     struct infw_v6_rec rec[INFW_BUCKET_INLINE];
 };
 
-// Two-choice slot form of the same groups (b2n = bucket count != 0), an opt-in alternative (INFW_V6_FORM=b2;
-// measured slower than the form above at configs[4], tables.cpp): it packs a group set into fewer 128-B lines
-// than one group per bucket at 1/8 load, for a table that could stay in the XCD L2s.  A
-// 64-B bucket holds two 32-B slots {tag, top, info, pad, record}; a group of one record takes one slot, a
-// group of two records both slots of one bucket (longest first), a larger group one slot with n =
-// INFW_BUCKET_OVERFLOW (Waldvogel table).  A group lives in bucket i1 or — when i1 was full — i2 (two
-// halves of one hash, range-reduced), and then i1's slot 0 carries INFW_B2_DISPLACED, so a lookup reads a
-// second bucket only for groups (or absent keys) whose first bucket overflowed.  Slot 1 is used only when
-// slot 0 is (an incremental removal moves slot 1 down); an emptied slot 0 keeps the bucket's DISPLACED flag.
-struct infw_v6_slot {       // 32 B
-    uint32_t tag;           // slot + 1, 0 = empty
-    uint32_t top;           // address bits 0..31
-    uint32_t info;          // records of the group (1, 2) or INFW_BUCKET_OVERFLOW; slot 0: | INFW_B2_DISPLACED
-    uint32_t pad;
-    struct infw_v6_rec rec;
-};
-#define INFW_B2_DISPLACED 0x80000000u
-// bucket index of a 32-bit hash half in [0, nb)
-#define INFW_B2_INDEX(h32, nb) ((uint64_t)(uint32_t)(h32) * (uint64_t)(nb) >> 32)
-
 // First-match decision tables.  For one (rule list, packet class) the
 // first-match result as a function of the 16-bit packet value (dport, or
 // type << 8 | code) is a step function with S <= 2c + 1 <= 201 segments.  The
@@ -179,17 +159,15 @@ struct infw_dev_tables {
     uint32_t n_wild;           // longest first; consulted for ifindexes without a slot (their own entries)
     uint32_t lean;             // 1: no compressed short table, no overflowed IPv6 group, no partial-ifindex prefix —
                                // the kernel may launch without those code paths (fewer live registers)
-    uint64_t b2n;              // != 0: btab holds the two-choice slot form with this many buckets
     const uint32_t *dt_pl;     // n_dt_pl != 0: per-list part counts, 3 bits per class (see infw_dt_slot_p)
     uint32_t n_dt_pl;
     uint32_t stat_flush_tiles;  // classify: a workgroup flushes its LDS counters every this many tiles (<= 1024)
-    const uint32_t *dxr_idx;   // short_mode INFW_SHORT_DXR: n_slots << 16 index words
-    const struct infw_dt_line *dxr_lines;
     const uint64_t *d16;       // d16_on: n_slots << 16 words in front of DIR-24-8 (INFW_D16_*)
     uint32_t d16_on;
     uint32_t dt_half;          // read decision lines half-first (the second 32 B only where needed; choose_dt_half)
     uint32_t split;            // classify in two phases (LPM -> per-packet decision-line address; then the decision
                                // lines as independent gathers): epochs whose entry lines span GiBs (classify.hip)
+    uint64_t n_dte;            // entry lines (host-side: the split decision)
 };
 
 INFW_TD uint32_t infw_bswap32(uint32_t x) {
@@ -393,15 +371,6 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 #define INFW_SHORT_DIR24 0u
 #define INFW_SHORT_COMPRESSED 1u
 #define INFW_SHORT_NONE 2u        // DIR-24-8 build without any <= /32 entry
-#define INFW_SHORT_DXR 3u         // range form: per /16 chunk one answer or one line of <= 11 ranges
-// Range form of the short table (DXR-style): per (slot, address bits 0..15) an index word holding either the
-// chunk's single answer (INFW_DXR_DIRECT | list+1) or the index of a 64-B range line: the chunk's <= 11 runs at
-// /32 granularity as 10 u16 keys in w[0..4] (key j = start of run j+1 minus 1, pad 0xFFFF, so "key < v" <=>
-// "run j+1 starts at or below v") and the runs' answers in w[5..15].  A lookup is the index word (L2-resident:
-// 256 KiB per slot) and at most one line per chunk, where DIR-24-8 spreads a /16../23 prefix over up to 16 lines.
-#define INFW_DXR_DIRECT 0x80000000u
-#define INFW_DXR_RUNS 11u
-
 // DIR-24-8 word (8 B).  Bits 63..62:
 //   00  plain: list+1 of the whole /24 in bits 0..31;
 //   10  tbl8 group index in bits 0..31 (256 u32 values, one per last byte);
@@ -421,11 +390,10 @@ INFW_TD uint32_t infw_node_child(const T &t, const struct infw_bnode &n, uint32_
 #define INFW_D24_MAXV 0x7FFFu
 #define INFW_D24_ABA_MAXV 0x3FFFFFu
 
-// Word for a /24 whose 256 values are g (tbl8 group gidx): inline when it can be
-// (and allow_inline; 0 keeps every group in tbl8, for A/B measurements).
-INFW_TD uint64_t infw_d24_encode(const uint32_t *g, uint32_t gidx, bool allow_inline = true) {
+// Word for a /24 whose 256 values are g (tbl8 group gidx): inline when it can be.
+INFW_TD uint64_t infw_d24_encode(const uint32_t *g, uint32_t gidx) {
     uint32_t v[3] = {g[0], 0, 0}, b[2] = {0, 0}, runs = 1;
-    bool ok = allow_inline;
+    bool ok = true;
     for (uint32_t x = 1; x < 256 && ok; x++) {
         if (g[x] == g[x - 1]) continue;
         if (runs == 3) ok = false;
@@ -529,35 +497,12 @@ INFW_TD uint32_t infw_long_lookup(const T &t, uint32_t slot, uint64_t hi, uint64
     return best;
 }
 
-// infw_v6_long over the two-choice slot form.
-template <class T>
-INFW_TD uint32_t infw_v6_long_b2(const T &t, uint32_t slot, uint32_t a32, uint32_t mid, uint64_t lo) {
-    const uint64_t h = infw_bucket_hash(slot, a32);
-    const struct infw_v6_slot *s = (const struct infw_v6_slot *)(const void *)t.btab;
-    for (int probe = 0; probe < 2; probe++) {
-        const struct infw_v6_slot *b = s + 2 * INFW_B2_INDEX(probe ? h : h >> 32, t.b2n);
-        for (int k = 0; k < 2; k++) {
-            if (b[k].tag == slot + 1 && b[k].top == a32) {
-                const uint32_t nr = b[k].info & 0xFFu;
-                if (nr == INFW_BUCKET_OVERFLOW) return infw_long_lookup(t, slot, (uint64_t)a32 << 32 | mid, lo);
-                if (infw_rec_match(b[k].rec.mid, b[k].rec.lo, b[k].rec.meta, mid, lo)) return b[k].rec.meta & 0x1FFFFFFu;
-                if (nr == 2 && k == 0 && infw_rec_match(b[1].rec.mid, b[1].rec.lo, b[1].rec.meta, mid, lo))
-                    return b[1].rec.meta & 0x1FFFFFFu;
-                return 0;
-            }
-        }
-        if (!(b[0].info & INFW_B2_DISPLACED)) return 0;  // (an emptied slot 0 keeps the bucket's flag)
-    }
-    return 0;
-}
-
 // Longest long (/33../128) prefix covering an IPv6 address: its /32 group's
 // bucket, or the Waldvogel table when the group overflowed.  list+1 or 0.
 template <class T>
 INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uint32_t sa[4]) {
     const uint32_t mid = infw_bswap32(sa[1]);
     const uint64_t lo = infw_be64(sa[2], sa[3]);
-    if (t.b2n) return infw_v6_long_b2(t, slot, a32, mid, lo);
     uint64_t i = infw_bucket_hash(slot, a32) & t.bmask;
     for (;;) {
         const struct infw_v6_bucket *b = &t.btab[i];
@@ -577,17 +522,8 @@ INFW_TD uint32_t infw_v6_long(const T &t, uint32_t slot, uint32_t a32, const uin
 }
 
 template <class T>
-INFW_TD uint32_t infw_dxr_lookup(const T &t, uint32_t slot, uint32_t a32) {
-    const uint32_t w = t.dxr_idx[((uint64_t)slot << 16) | (a32 >> 16)];
-    if (w & INFW_DXR_DIRECT) return w & ~INFW_DXR_DIRECT;
-    const uint32_t *l = t.dxr_lines[w].w;
-    return l[5 + infw_keys_below(l, 0, 5, a32 & 0xFFFFu)];
-}
-
-template <class T>
 INFW_TD uint32_t infw_short_lookup(const T &t, uint32_t slot, uint32_t a32) {
     if (t.short_mode == INFW_SHORT_DIR24) return t.d16_on ? infw_d16_lookup(t, slot, a32) : infw_dir24_lookup(t, slot, a32);
-    if (t.short_mode == INFW_SHORT_DXR) return infw_dxr_lookup(t, slot, a32);
     return t.short_mode == INFW_SHORT_COMPRESSED ? infw_dir_lookup(t, slot, a32) : 0u;
 }
 

@@ -498,18 +498,11 @@ static void fill_leaf(infw_dt_line &l, const uint32_t *starts, const uint32_t *r
     }
 }
 
-// INFW_DT_FORM=wide keeps every leaf in the u32 form (A/B measurements).
-static bool dt_compact_allowed() {
-    const char *e = getenv("INFW_DT_FORM");
-    return !(e && strcmp(e, "wide") == 0);
-}
-
-// Host threads for compiling rule lists (INFW_COMPILE_THREADS overrides; lists are independent, so a
+// Host threads for compiling rule lists (Options::compile_threads overrides; lists are independent, so a
 // compile of 1M distinct 99-rule lists scales with cores).  Small sets stay on the calling thread.
-static int compile_threads(size_t n_items) {
+static int compile_threads(size_t n_items, int req) {
     if (n_items < 4096) return 1;
-    int t = (int)std::thread::hardware_concurrency();
-    if (const char *e = getenv("INFW_COMPILE_THREADS")) t = atoi(e);
+    const int t = req > 0 ? req : (int)std::thread::hardware_concurrency();
     return std::max(1, std::min(t, 16));
 }
 
@@ -528,7 +521,7 @@ static void parallel_chunks(size_t n, int nt, F f) {
 int emit_decision_lines(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, infw_dt_line &entry,
                         std::vector<infw_dt_line> &leaves) {
     const uint32_t S = (uint32_t)starts.size();
-    bool compact = dt_compact_allowed();
+    bool compact = true;
     for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
     const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
     memset(&entry, 0, sizeof(entry));
@@ -661,8 +654,8 @@ static void class_records(const uint8_t *val, std::vector<uint64_t> per[INFW_NCL
 // line.  Fewer parts = fewer entry lines = more of them resident in L2: a rule set of short
 // lists (configs[1]: 10 rules) fits one line per (list, class) — 1/16 of the footprint —
 // while 99-rule lists (configs[2]) need 16 parts to stay at one line per packet.
-static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
-    const int nt = compile_threads(vals.size());
+static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals, const Options &opt) {
+    const int nt = compile_threads(vals.size(), opt.compile_threads);
     std::vector<std::array<uint64_t, 10>> acc(nt);  // per thread: lines[5], over[5]
     parallel_chunks(vals.size(), nt, [&](int t, size_t a, size_t b) {
         uint64_t *lines = acc[t].data(), *over = lines + 5;
@@ -674,7 +667,7 @@ static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
             class_records(vals[x], per);
             for (int c = 0; c < INFW_NCLS; c++) {
                 step_function(per[c], starts, res);
-                bool compact = dt_compact_allowed();
+                bool compact = true;
                 for (uint32_t r : res) compact = compact && infw_dt_result_code(r) <= 0xFFu;
                 const uint32_t segs = compact ? INFW_DT_CLEAF_SEGS : INFW_DT_LEAF_SEGS;
                 for (uint32_t pl = 0; pl <= 4; pl++) {
@@ -700,7 +693,7 @@ static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
             lines[pl] += a[pl];
             over[pl] += a[5 + pl];
         }
-    if (getenv("INFW_COMPILE_TRACE"))
+    if (opt.trace & 1)
         for (uint32_t pl = 0; pl <= 4; pl++)
             fprintf(stderr, "[compile] %u parts: %llu (list, class, part) lines, %llu need a root + leaf\n", 1u << pl,
                     (unsigned long long)lines[pl], (unsigned long long)over[pl]);
@@ -712,14 +705,13 @@ static uint32_t choose_dt_plog2(const std::vector<const uint8_t *> &vals) {
 // Does every one of the 2^p parts of a step function fit one decision line (no root)?  Mirrors
 // emit_decision_lines' forms: a compact leaf holds 20 segments when all of the part's results have a code.
 static bool parts_fit_one_line(const std::vector<uint32_t> &starts, const std::vector<uint32_t> &res, uint32_t p) {
-    const bool compact_ok = dt_compact_allowed();
     const uint32_t span = 65536u >> p;
     size_t j = 0;
     for (uint32_t q = 0; q < (1u << p); q++) {
         const uint32_t lo = q * span, hi = lo + span;
         while (j + 1 < starts.size() && starts[j + 1] <= lo) j++;
         uint32_t S = 1;
-        bool compact = compact_ok && infw_dt_result_code(res[j]) <= 0xFFu;
+        bool compact = infw_dt_result_code(res[j]) <= 0xFFu;
         for (size_t k = j + 1; k < starts.size() && starts[k] < hi; k++) {
             S++;
             compact = compact && infw_dt_result_code(res[k]) <= 0xFFu;
@@ -817,9 +809,9 @@ static void reserve_slack(V &v, size_t n, bool inc) {
     v.reserve(inc ? n + std::max<size_t>(n / 4, 4096) : n);
 }
 
-int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uint64_t dir24_budget, IncState *inc) {
-    // INFW_COMPILE_TRACE=1: wall time per phase on stderr
-    const bool trace = getenv("INFW_COMPILE_TRACE") != nullptr;
+int compile_tables(const PendingMap &m, HostTables &out, const Options &opt, IncState *inc) {
+    // Options::trace & 1: wall time per phase on stderr
+    const bool trace = (opt.trace & 1) != 0;
     auto tp = std::chrono::steady_clock::now();
     auto phase = [&](const char *what) {
         if (!trace) return;
@@ -912,15 +904,14 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         std::vector<const uint8_t *> vals;
         vals.reserve(list_of_vid.size());
         for (const auto &p : list_of_vid) vals.push_back(m.pool.vals[p.first].data());
-        out.dt_plog2 = choose_dt_plog2(vals);
-        uint64_t budget = 2ull << 30;
-        if (const char *e = getenv("INFW_DT_BUDGET_MB")) budget = strtoull(e, nullptr, 10) << 20;
+        out.dt_plog2 = choose_dt_plog2(vals, opt);
+        const uint64_t budget = (uint64_t)opt.dt_budget_mb << 20;
         while (out.dt_plog2 && ((uint64_t)out.n_lists * INFW_NCLS * sizeof(infw_dt_line) << out.dt_plog2) > budget)
             out.dt_plog2--;
     }
     phase("choose parts");
-    if (const char *e = getenv("INFW_DT_PARTS")) {
-        const int v = atoi(e);
+    if (opt.dt_parts) {
+        const int v = opt.dt_parts;
         out.dt_plog2 = v == 16 ? 4 : v == 8 ? 3 : v == 4 ? 2 : v == 2 ? 1 : v == 1 ? 0 : out.dt_plog2;
     }
     reserve_slack(out.dte, ((size_t)std::max<uint32_t>(out.n_lists, 1) * INFW_NCLS) << out.dt_plog2, inc);
@@ -933,15 +924,14 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         // entries' leaf index) rebased — the image is identical to a serial compile
         std::vector<uint32_t> vid_of_lid(out.n_lists);
         for (const auto &p : list_of_vid) vid_of_lid[p.second] = p.first;
-        const int nt = compile_threads(out.n_lists);
+        const int nt = compile_threads(out.n_lists, opt.compile_threads);
         std::vector<std::vector<uint64_t>> rules_t(nt);
         std::vector<std::vector<infw_dt_line>> leaves_t(nt);
         std::vector<int> rc_t(nt, 0);
         std::vector<std::pair<size_t, size_t>> range_t(nt);
         const size_t ents = (size_t)INFW_NCLS << out.dt_plog2;
-        // per-list part counts when the list count fits the kernel's LDS copy (INFW_DT_ADAPT=0 turns them off)
-        const char *ea = getenv("INFW_DT_ADAPT");
-        const bool adapt = out.dt_plog2 > 0 && out.n_lists <= INFW_DT_PL_LISTS && !(ea && atoi(ea) == 0);
+        // per-list part counts when the list count fits the kernel's LDS copy (Options::dt_adapt 0 turns them off)
+        const bool adapt = out.dt_plog2 > 0 && out.n_lists <= INFW_DT_PL_LISTS && opt.dt_adapt != 0;
         out.dt_pl.assign(adapt ? INFW_DT_PL_LISTS : 0, 0u);
         parallel_chunks(out.n_lists, nt, [&](int t, size_t a, size_t b) {
             range_t[t] = {a, b};
@@ -1051,15 +1041,11 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     std::sort(shorts.begin(), shorts.end(), [](const ShortEnt &a, const ShortEnt &b) {
         return a.slot != b.slot ? a.slot < b.slot : a.plen < b.plen;
     });
-    out.short_mode = short_mode_req >= 0 ? (uint32_t)short_mode_req
-                     : ((uint64_t)out.n_slots << 27) <= dir24_budget ? INFW_SHORT_DIR24 : INFW_SHORT_COMPRESSED;
-    // the range form is derived from the DIR-24-8 build image (kept as well: incremental commits patch that)
-    bool dxr = out.short_mode == INFW_SHORT_DXR;
-    if (dxr) out.short_mode = INFW_SHORT_DIR24;
-    out.dxr_idx.clear();
-    out.dxr_lines.clear();
+    // DIR-24-8 (128 MiB of words per ifindex) while the ifindexes' words fit 4 GiB, else the compressed form
+    out.short_mode = opt.short_table == 1 ? INFW_SHORT_COMPRESSED
+                     : opt.short_table == 0 || ((uint64_t)out.n_slots << 27) <= (4ull << 30) ? INFW_SHORT_DIR24
+                                                                                          : INFW_SHORT_COMPRESSED;
     const bool dir24 = out.short_mode == INFW_SHORT_DIR24;
-    if (const char *e = getenv("INFW_D24_INLINE")) out.d24_inline = atoi(e) != 0;
     out.l16.assign(dir24 ? 1 : (size_t)std::max<uint32_t>(out.n_slots, 1) << 16, 0u);
     {
         std::vector<uint32_t> t24, t8;
@@ -1120,49 +1106,13 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
                     const uint32_t w = t24[k];
                     if (w & INFW_TBL8_FLAG) {
                         const uint32_t lg = w & ~INFW_TBL8_FLAG;
-                        out.tbl24[((size_t)slot << 24) + k] = infw_d24_encode(&t8[(size_t)lg << 8], gbase + lg, out.d24_inline);
+                        out.tbl24[((size_t)slot << 24) + k] = infw_d24_encode(&t8[(size_t)lg << 8], gbase + lg);
                         out.tbl8_of[(uint64_t)slot << 24 | k] = gbase + lg;
                     } else {
                         out.tbl24[((size_t)slot << 24) + k] = w;
                     }
                 }
                 out.tbl8.insert(out.tbl8.end(), t8.begin(), t8.end());
-                if (dxr) {  // the runs of every /16 chunk at /32 granularity; > INFW_DXR_RUNS anywhere: no range form
-                    if (out.dxr_idx.empty()) out.dxr_idx.assign((size_t)out.n_slots << 16, INFW_DXR_DIRECT);
-                    uint32_t rs[INFW_DXR_RUNS], rv[INFW_DXR_RUNS];
-                    for (uint32_t b = 0; b < 65536 && dxr; b++) {
-                        uint32_t nr = 0;
-                        auto push = [&](uint32_t start, uint32_t v) {
-                            if (nr && rv[nr - 1] == v) return true;
-                            if (nr == INFW_DXR_RUNS) return false;
-                            rs[nr] = start;
-                            rv[nr++] = v;
-                            return true;
-                        };
-                        for (uint32_t i = 0; i < 256 && dxr; i++) {
-                            const uint32_t w = t24[((size_t)b << 8) | i];
-                            if (w & INFW_TBL8_FLAG) {
-                                const uint32_t *g = &t8[(size_t)(w & ~INFW_TBL8_FLAG) << 8];
-                                for (uint32_t x = 0; x < 256 && dxr; x++) dxr = push(i << 8 | x, g[x]);
-                            } else {
-                                dxr = push(i << 8, w);
-                            }
-                        }
-                        if (!dxr) break;
-                        uint32_t &iw = out.dxr_idx[((size_t)slot << 16) | b];
-                        if (nr == 1) {
-                            iw = INFW_DXR_DIRECT | rv[0];
-                            continue;
-                        }
-                        infw_dt_line l;
-                        uint16_t key[10];
-                        for (uint32_t j = 0; j < 10; j++) key[j] = j + 1 < nr ? (uint16_t)(rs[j + 1] - 1) : (uint16_t)0xFFFF;
-                        for (uint32_t k = 0; k < 5; k++) l.w[k] = (uint32_t)key[2 * k] | (uint32_t)key[2 * k + 1] << 16;
-                        for (uint32_t j = 0; j < INFW_DXR_RUNS; j++) l.w[5 + j] = j < nr ? rv[j] : 0u;
-                        iw = (uint32_t)out.dxr_lines.size();
-                        out.dxr_lines.push_back(l);
-                    }
-                }
                 si = sj;
                 continue;
             }
@@ -1186,21 +1136,12 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     if (out.tbl24.empty()) {  // no <= /32 entry on any interface: nothing to index
         out.tbl24.push_back(0);
         if (out.short_mode == INFW_SHORT_DIR24) out.short_mode = INFW_SHORT_NONE;
-        dxr = false;
-    }
-    if (dxr && !out.dxr_idx.empty()) {
-        out.short_mode = INFW_SHORT_DXR;
-    } else {
-        out.dxr_idx.clear();
-        out.dxr_lines.clear();
     }
     {
         uint64_t n_wide = 0;  // <= /32 prefixes of /20 or shorter
         for (const ShortEnt &e : shorts) n_wide += e.plen <= 20;
-        build_d16(out, shorts.size(), n_wide);
+        build_d16(out, shorts.size(), n_wide, opt.d16);
     }
-    if (out.dxr_idx.empty()) out.dxr_idx.push_back(INFW_DXR_DIRECT);
-    if (out.dxr_lines.empty()) out.dxr_lines.push_back(infw_dt_line{});
     if (out.tbl8.empty()) out.tbl8.assign(256, 0);
     if (out.nodes.empty()) out.nodes.push_back(infw_bnode{});
     if (out.vpool.empty()) out.vpool.push_back(0);
@@ -1286,120 +1227,15 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
             }
             g.recs.push_back(infw_v6_rec{r.lo, (uint32_t)r.hi, (r.len - 32) << 25 | r.list1});
         }
-        // the two-choice slot form (infw_tables.h) only when INFW_V6_FORM=b2 asks for it: from 70 % slot load,
-        // the table grown by 1/8 while a cuckoo placement fails.  Measured slower than one group per bucket at
-        // configs[4], the workload it was built for (3.99 vs 3.85 ms, profiles/r02h3/ab_v6form_cfg4.txt): the
-        // two-record groups hold the placement to ~50 % slot load (6.8 MB for 80k groups), and slot-1 and
-        // second-bucket reads cost more than the misses the denser table saves.
-        {
-            const char *fe = getenv("INFW_V6_FORM");
-            const bool force_b2 = fe && !strcmp(fe, "b2"), force_std = !force_b2;
-            std::vector<uint64_t> keys;
-            keys.reserve(groups.size());
-            uint64_t slots = 0;
-            for (const auto &kv : groups) {
-                keys.push_back(kv.first);
-                slots += kv.second.recs.size() == 2 ? 2 : 1;
-            }
-            std::sort(keys.begin(), keys.end());
-            uint64_t nb = std::max<uint64_t>(64, (slots * 5 + 6) / 7);  // 2 slots per bucket at 70 % load
-            const bool want = !groups.empty() && !force_std;
-            for (int attempt = 0; want && attempt < 8; attempt++, nb += nb / 8) {
-                std::vector<infw_v6_slot> tab(2 * nb);
-                memset(tab.data(), 0, tab.size() * sizeof(infw_v6_slot));
-                auto idx = [&](const G &g, int which) {
-                    const uint64_t h = infw_bucket_hash(g.slot, g.top);
-                    return which ? INFW_B2_INDEX(h, nb) : INFW_B2_INDEX(h >> 32, nb);
-                };
-                auto need_of = [](const G &g) -> uint32_t { return g.recs.size() == 2 ? 2u : 1u; };
-                auto put = [&](uint64_t i, G &g) {  // into bucket i's free slots, or false
-                    infw_v6_slot *b = &tab[2 * i];
-                    const uint32_t k = b[0].tag == 0 ? 0 : b[1].tag == 0 ? 1 : 2, need = need_of(g);
-                    if (k + need > 2) return false;
-                    if (g.recs.size() > 2) {
-                        b[k].info = INFW_BUCKET_OVERFLOW;
-                    } else {
-                        std::sort(g.recs.begin(), g.recs.end(),
-                                  [](const infw_v6_rec &x, const infw_v6_rec &y) { return x.meta > y.meta; });
-                        for (uint32_t j = 0; j < need; j++) {
-                            b[k + j].info = (uint32_t)g.recs.size();
-                            b[k + j].rec = g.recs[j];
-                        }
-                    }
-                    for (uint32_t j = 0; j < need; j++) {
-                        b[k + j].tag = g.slot + 1;
-                        b[k + j].top = g.top;
-                    }
-                    return true;
-                };
-                // cuckoo insertion: a group that finds both buckets full evicts the groups of one of them
-                // (chosen by a fixed-seed generator), which are re-inserted in turn, up to a step limit
-                uint64_t rng = 0x9E3779B97F4A7C15ull, steps = 0;
-                const uint64_t max_steps = 64 * groups.size() + 1024;
-                bool ok = true;
-                std::vector<uint64_t> pending;
-                for (int pass = 0; pass < 2 && ok; pass++)  // two-record groups (a whole bucket) first
-                    for (uint64_t key : keys) {
-                        if ((groups[key].recs.size() == 2) != (pass == 0)) continue;
-                        pending.push_back(key);
-                        while (!pending.empty() && ok) {
-                            const uint64_t cur = pending.back();
-                            pending.pop_back();
-                            G &g = groups[cur];
-                            if (put(idx(g, 0), g) || put(idx(g, 1), g)) continue;
-                            if (++steps > max_steps) {
-                                ok = false;
-                                break;
-                            }
-                            rng = rng * 6364136223846793005ull + 1442695040888963407ull;
-                            const uint64_t v = idx(g, (int)(rng >> 63));
-                            infw_v6_slot *b = &tab[2 * v];
-                            const bool pair = b[0].tag == b[1].tag && b[0].top == b[1].top;  // one two-slot group
-                            if (need_of(g) == 2 || pair) {  // evict the bucket's groups (a two-slot group once)
-                                for (int k = 0; k < (pair ? 1 : 2); k++)
-                                    if (b[k].tag) pending.push_back((uint64_t)(b[k].tag - 1) << 32 | b[k].top);
-                                b[0] = b[1] = infw_v6_slot{};
-                            } else {  // one slot, chosen at random: the other group stays (moved to slot 0)
-                                const int k = (int)(rng >> 62) & 1;
-                                pending.push_back((uint64_t)(b[k].tag - 1) << 32 | b[k].top);
-                                if (k == 0) b[0] = b[1];
-                                b[0].info &= ~INFW_B2_DISPLACED;
-                                b[1] = infw_v6_slot{};
-                            }
-                            put(v, g);
-                        }
-                    }
-                if (ok)  // a group living in its second bucket marks its first one
-                    for (uint64_t i = 0; i < nb; i++)
-                        for (int k = 0; k < 2; k++) {
-                            const infw_v6_slot &sl = tab[2 * i + k];
-                            if (!sl.tag || (k == 1 && tab[2 * i].tag == sl.tag && tab[2 * i].top == sl.top)) continue;
-                            const uint64_t i1 = idx(groups[(uint64_t)(sl.tag - 1) << 32 | sl.top], 0);
-                            if (i1 != i) tab[2 * i1].info |= INFW_B2_DISPLACED;
-                        }
-                if (trace)
-                    fprintf(stderr, "[compile] IPv6 slot form: %zu groups, %llu slots, %llu buckets: %s\n", groups.size(),
-                            (unsigned long long)slots, (unsigned long long)nb, ok ? "placed" : "placement failed");
-                if (!ok) continue;
-                out.btab.assign(nb, infw_v6_bucket{});
-                memcpy(out.btab.data(), tab.data(), nb * sizeof(infw_v6_bucket));
-                out.b2n = nb;
-                for (const auto &kv : groups) out.n_overflow_groups += kv.second.recs.size() > 2;
-                break;
-            }
-        }
-        // a wave waits for its slowest lane's probe chain: keep the load at or below 1/8
-        // (INFW_BUCKET_SPREAD=k: capacity >= k x groups), the untouched capacity costs no cache
-        uint64_t spread = 8;
-        if (const char *e = getenv("INFW_BUCKET_SPREAD")) spread = std::max(2, atoi(e));
+        // a wave waits for its slowest lane's probe chain: keep the load at or below 1/8 (the untouched capacity
+        // costs no cache)
+        const uint64_t spread = 8;
         uint64_t cap = 1024;
         while (cap < groups.size() * spread) cap <<= 1;
-        if (out.b2n) cap = 0;  // placed in the slot form above
-        if (cap) out.btab.assign(cap, infw_v6_bucket{});
-        if (cap) memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
+        out.btab.assign(cap, infw_v6_bucket{});
+        memset(out.btab.data(), 0, cap * sizeof(infw_v6_bucket));
         const uint64_t bmask = cap - 1;
         for (auto &kv : groups) {
-            if (!cap) break;
             G &g = kv.second;
             uint64_t i = infw_bucket_hash(g.slot, g.top) & bmask;
             while (out.btab[i].tag) i = (i + 1) & bmask;
@@ -1420,7 +1256,8 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
         out.n_buckets = groups.size();
     }
     phase("buckets");
-    out.dt_half = choose_dt_half(out);
+    out.dt_short_lines = count_dt_short_lines(out);
+    out.dt_half = choose_dt_half(out, opt.dt_half);
     if (inc) {
         // the buffers incremental commits append to get the device images' 25 % slack on the host too, so
         // the first commits after a compile do not copy a 30-MB vector to grow it by one rule list
@@ -1447,16 +1284,19 @@ int compile_tables(const PendingMap &m, HostTables &out, int short_mode_req, uin
     return 0;
 }
 
-uint32_t choose_dt_half(const HostTables &h) {
+uint32_t choose_dt_half(const HostTables &h, int req) {
     // the kernel's decision-line reads (infw_dev_tables.dt_half): the first 32 B, then the second half only where
     // needed, when nearly every entry line is a compact leaf of <= 9 segments (answered by its first half: configs[1],
     // same-box A/B 1.107 -> 1.020 ms); else the whole line at once (a wave waits for the dependent second half
     // whenever one of its lanes needs it: configs[2] and [4] 0.2-0.5 % slower reading halves, profiles/r04hf)
-    if (const char *e = getenv("INFW_DT_HALF")) return atoi(e) ? 1u : 0u;
-    uint64_t short_lines = 0;
-    for (const infw_dt_line &l : h.dte)
-        short_lines += (l.w[0] & INFW_DT_COMPACT) && !(l.w[0] & INFW_DT_ROOT) && (l.w[0] & 0xFFu) <= 9;
-    return !h.dte.empty() && short_lines * 100 >= (uint64_t)h.dte.size() * 95 ? 1u : 0u;
+    if (req >= 0) return req ? 1u : 0u;
+    return !h.dte.empty() && h.dt_short_lines * 100 >= (uint64_t)h.dte.size() * 95 ? 1u : 0u;
+}
+
+uint64_t count_dt_short_lines(const HostTables &h) {
+    uint64_t n = 0;
+    for (const infw_dt_line &l : h.dte) n += infw_dt_line_short(l);
+    return n;
 }
 
 uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *runs) {
@@ -1493,12 +1333,10 @@ uint64_t d16_word(const HostTables &h, uint32_t slot, uint32_t hi, uint32_t *run
     return infw_d16_encode(v[0], v[1], st[1], nr == 3 ? st[2] - 1 : 0xFFFFu);
 }
 
-void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide) {
+void build_d16(HostTables &h, uint64_t n_short, uint64_t n_short_wide, int req) {
     h.d16_on = 0;
     h.d16_permille = 0;
     h.d16.clear();
-    const char *env = getenv("INFW_D16");
-    const int req = env ? atoi(env) : -1;
     if (h.short_mode == INFW_SHORT_DIR24 && h.tbl24.size() == ((size_t)h.n_slots << 24) && h.n_slots && req != 0) {
         std::vector<uint64_t> d((size_t)h.n_slots << 16);
         std::vector<uint64_t> cnt(2 * (size_t)h.n_slots, 0);  // per slot: /16s with structure, of them inline
@@ -1562,8 +1400,6 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
     case TB_LEVELS: INFW_HB(levels);
     case TB_WILD: INFW_HB(wild);
     case TB_DTPL: INFW_HB(dt_pl);
-    case TB_DXRI: INFW_HB(dxr_idx);
-    case TB_DXRL: INFW_HB(dxr_lines);
     case TB_D16: INFW_HB(d16);
     default:
         *p = nullptr;
@@ -1572,43 +1408,55 @@ void host_buffer(const HostTables &h, int b, const void **p, size_t *bytes) {
 #undef INFW_HB
 }
 
-infw_dev_tables HostTables::view() const {
+infw_dev_tables view_of(const HostTables &h, void *const buf[TB_COUNT]) {
     infw_dev_tables t;
     memset(&t, 0, sizeof(t));
-    t.wild = wild.data();
-    t.n_wild = n_wild;
-    t.lean = (short_mode == INFW_SHORT_DIR24 || short_mode == INFW_SHORT_NONE || short_mode == INFW_SHORT_DXR) && n_overflow_groups == 0 && n_wild == 0;
-    t.if_keys = if_keys.data();
-    t.if_slot = if_slot.data();
-    t.if_mask = (uint32_t)if_keys.size() - 1;
-    t.if_mult = if_mult;
-    t.if_shift = if_shift;
-    t.n_slots = n_slots;
-    t.l16 = l16.data();
-    t.tbl24 = tbl24.data();
-    t.tbl8 = tbl8.data();
-    t.short_mode = short_mode;
-    t.nodes = nodes.data();
-    t.vpool = vpool.data();
-    t.ltab = ltab.data();
-    t.lmask = ltab.size() - 1;
-    t.btab = btab.data();
-    t.bmask = btab.size() - 1;
-    t.b2n = b2n;
-    t.desc = desc.data();
-    t.rules = rules.data();
-    t.dte = dte.data();
-    t.dtl = dtl.data();
-    t.n_levels = (uint32_t)levels.size();
-    t.levels = levels.data();
-    t.dt_plog2 = dt_plog2;
-    t.dt_pl = dt_pl.data();
-    t.n_dt_pl = (uint32_t)dt_pl.size();
-    t.dxr_idx = dxr_idx.data();
-    t.dxr_lines = dxr_lines.data();
-    t.d16 = d16.data();
-    t.d16_on = d16_on;
+    t.if_keys = static_cast<const uint32_t *>(buf[TB_IFK]);
+    t.if_slot = static_cast<const uint32_t *>(buf[TB_IFS]);
+    t.l16 = static_cast<const uint32_t *>(buf[TB_L16]);
+    t.nodes = static_cast<const infw_bnode *>(buf[TB_NODES]);
+    t.vpool = static_cast<const uint32_t *>(buf[TB_VPOOL]);
+    t.tbl24 = static_cast<const uint64_t *>(buf[TB_TBL24]);
+    t.tbl8 = static_cast<const uint32_t *>(buf[TB_TBL8]);
+    t.ltab = static_cast<const infw_long_entry *>(buf[TB_LTAB]);
+    t.btab = static_cast<const infw_v6_bucket *>(buf[TB_BTAB]);
+    t.desc = static_cast<const uint64_t *>(buf[TB_DESC]);
+    t.rules = static_cast<const uint64_t *>(buf[TB_RULES]);
+    t.dte = static_cast<const infw_dt_line *>(buf[TB_DTE]);
+    t.dtl = static_cast<const infw_dt_line *>(buf[TB_DTL]);
+    t.levels = static_cast<const uint8_t *>(buf[TB_LEVELS]);
+    t.wild = static_cast<const uint32_t *>(buf[TB_WILD]);
+    t.dt_pl = static_cast<const uint32_t *>(buf[TB_DTPL]);
+    t.d16 = static_cast<const uint64_t *>(buf[TB_D16]);
+    t.n_wild = h.n_wild;
+    t.lean = (h.short_mode == INFW_SHORT_DIR24 || h.short_mode == INFW_SHORT_NONE) && h.n_overflow_groups == 0 &&
+             h.n_wild == 0;
+    t.if_mask = (uint32_t)h.if_keys.size() - 1;
+    t.if_mult = h.if_mult;
+    t.if_shift = h.if_shift;
+    t.n_slots = h.n_slots;
+    t.short_mode = h.short_mode;
+    t.lmask = h.ltab.size() - 1;
+    t.bmask = h.btab.size() - 1;
+    t.n_levels = (uint32_t)h.levels.size();
+    t.dt_plog2 = h.dt_plog2;
+    t.n_dt_pl = (uint32_t)h.dt_pl.size();
+    t.d16_on = h.d16_on;
+    t.dt_half = h.dt_half;
+    t.n_dte = h.dte.size();
+    t.stat_flush_tiles = 1024;
     return t;
+}
+
+infw_dev_tables HostTables::view() const {
+    void *buf[TB_COUNT];
+    for (int b = 0; b < TB_COUNT; b++) {
+        const void *p;
+        size_t bytes;
+        host_buffer(*this, b, &p, &bytes);
+        buf[b] = const_cast<void *>(p);
+    }
+    return view_of(*this, buf);
 }
 
 }  // namespace infw

@@ -386,8 +386,10 @@ int infw_wl_line_rates(int dev, double *out) {
     hipEvent_t a = nullptr, b = nullptr;
     int rc = 0;
     if (hipMalloc(&tab, big) != hipSuccess || hipMalloc(&sink, sink_words * 4) != hipSuccess ||
-        hipMemset(tab, 1, big) != hipSuccess || hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+        hipMemset(tab, 1, big) != hipSuccess || hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
         rc = -ENOMEM;
+        (void)hipGetLastError();  // the failed allocation's sticky error must not surface in the caller's next check
+    }
     auto timed = [&](auto launch, int reps) -> double {  // ms per launch after one untimed launch
         launch();
         (void)hipEventRecord(a, 0);

@@ -119,8 +119,8 @@ class TableInfo(C.Structure):
                 ("device_bytes", C.c_uint64), ("compile_ms", C.c_double), ("upload_ms", C.c_double),
                 ("n_v6_groups", C.c_uint64), ("n_v6_overflow", C.c_uint64),
                 ("commit_mode", C.c_uint32), ("dt_parts", C.c_uint32), ("patch_bytes", C.c_uint64),
-                ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("v6_slot_buckets", C.c_uint64),
-                ("short_mode", C.c_uint32), ("dxr_lines", C.c_uint32),
+                ("dead_lists", C.c_uint64), ("full_reason", C.c_char * 48), ("reserved0", C.c_uint64),
+                ("short_mode", C.c_uint32), ("reserved1", C.c_uint32),
                 ("device_ms_max", C.c_double), ("n_device_slots", C.c_uint32), ("imported", C.c_uint32),
                 ("d16", C.c_uint32), ("d16_permille", C.c_uint32), ("split", C.c_uint32),
                 ("dt_half_reads", C.c_uint32), ("reserved", C.c_uint64 * 12)]
@@ -142,9 +142,12 @@ ABI_SYMBOLS = [
     "infw_host_register", "infw_host_unregister", "infw_classify_c", "infw_soa_compact", "infw_pack_frames_c", "infw_classify_frames",
     "infw_classify_frames_ex",
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
-    "infw_table_delete_batch",
+    "infw_table_delete_batch", "infw_set_option", "infw_get_option", "infw_option_name", "infw_classify_variant",
+    "infw_kernel_variant_name",
 ]
-ABI_VERSION = 3  # include/infw.h INFW_ABI_VERSION
+ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
+INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES = 0, 1, 2  # INFW_INPUT_*
+VARIANT_EVENTS = 0x1  # INFW_VARIANT_EVENTS
 
 
 # torch (device memory, streams, RCCL) ships its own libamdhip64.so.7; loading it
@@ -218,6 +221,11 @@ _sig = {
     "infw_build_id": (C.c_char_p, []),
     "infw_table_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "infw_table_import": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "infw_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
+    "infw_get_option": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
+    "infw_option_name": (C.c_char_p, [C.c_int]),
+    "infw_classify_variant": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]),
+    "infw_kernel_variant_name": (C.c_char_p, [C.c_int]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -287,6 +295,24 @@ for _name, (_res, _args) in _wsig.items():
 assert C.sizeof(EventHdrSt) == 8 and C.sizeof(EventRec) == 24
 if lib.infw_abi_version() != ABI_VERSION:
     raise ImportError(f"{LIB_PATH}: ABI {lib.infw_abi_version()}, these bindings are ABI {ABI_VERSION}: rebuild (make)")
+
+
+def option_names() -> list:
+    """Every per-context option the library knows (infw_option_name)."""
+    out, i = [], 0
+    while (n := lib.infw_option_name(i)) is not None:
+        out.append(n.decode())
+        i += 1
+    return out
+
+
+def kernel_variants() -> list:
+    """The registry of every kernel instantiation the library launches (infw_kernel_variant_name)."""
+    out, i = [], 0
+    while (n := lib.infw_kernel_variant_name(i)) is not None:
+        out.append(n.decode())
+        i += 1
+    return out
 
 
 def build_id() -> str:

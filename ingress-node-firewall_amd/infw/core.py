@@ -31,6 +31,12 @@ def key_from_fields(prefix_len: int, ifindex: int, ip: bytes) -> LpmIpKeySt:
     return k
 
 
+# Options applied to every Classifier created afterwards, before the caller's own `options` (include/infw.h
+# infw_set_option).  A process that wants one form everywhere (a tool, a test) sets them once; the library itself
+# reads no environment.
+DEFAULT_OPTIONS: Dict[str, int] = {}
+
+
 class Classifier:
     """One context = replicated GPU tables + one statistics slot per device.
 
@@ -38,11 +44,30 @@ class Classifier:
     debug_walk) that works without a GPU; classify() then raises ENODEV.
     """
 
-    def __init__(self, devices: Optional[Sequence[int]] = None, max_entries: int = 0, flags: int = 0):
+    def __init__(self, devices: Optional[Sequence[int]] = None, max_entries: int = 0, flags: int = 0,
+                 options: Optional[Dict[str, int]] = None):
         self._ctx = C.c_void_p()
         arr = (C.c_int * len(devices))(*devices) if devices else None
         check(N.lib.infw_create(C.byref(self._ctx), arr, len(devices) if devices else 0, max_entries, flags),
               "infw_create")
+        for k, v in {**DEFAULT_OPTIONS, **(options or {})}.items():
+            self.set_option(k, v)
+
+    # -- per-context options (include/infw.h infw_set_option): bit-exact table forms and launch choices
+    def set_option(self, name: str, value: int) -> None:
+        check(N.lib.infw_set_option(self._ctx, name.encode(), int(value)), f"set_option({name}={value})")
+
+    def option(self, name: str) -> int:
+        v = C.c_int64(0)
+        check(N.lib.infw_get_option(self._ctx, name.encode(), C.byref(v)), f"get_option({name})")
+        return v.value
+
+    def variant(self, input: int = N.INPUT_SOA, events: bool = False, dev: int = 0) -> str:
+        """Registry name of the kernel instantiation(s) a launch would run (infw_classify_variant)."""
+        buf = C.create_string_buffer(256)
+        check(N.lib.infw_classify_variant(self._ctx, dev, input, N.VARIANT_EVENTS if events else 0, buf, 256),
+              "classify_variant")
+        return buf.value.decode()
 
     # -- lifecycle
     def close(self):
@@ -170,7 +195,7 @@ class Classifier:
     def info(self) -> Dict[str, float]:
         ti = N.TableInfo()
         check(N.lib.infw_table_info(self._ctx, C.byref(ti)), "info")
-        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f not in ("pad0", "pad1", "reserved")}
+        d = {f: getattr(ti, f) for f, _ in N.TableInfo._fields_ if f not in ("reserved0", "reserved1", "reserved")}
         d["full_reason"] = ti.full_reason.decode()
         return d
 

@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
     assert sorted(N.ABI_SYMBOLS) == decl
     for name in decl:
         assert hasattr(N.lib, name), name
-    assert N.lib.infw_abi_version() == 3
+    assert N.lib.infw_abi_version() == 4
 
 
 def test_struct_sizes_match_reference_abi():

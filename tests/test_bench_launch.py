@@ -65,6 +65,29 @@ def test_gpus_2_spawns_two_ranks_same_digest():
     assert stats_digest(host_counters(c.debug_walk(t), t[:, 5])) == two["config"]["stats_digest"]
 
 
+def test_in_process_shape_same_digest_as_ranks():
+    """--in-process (one context, N slots, a host thread per slot; counters summed per rule over the slots) on a CPU
+    box: with --host-walk each slot's thread walks its shard through the shared host image concurrently; for the
+    same fixed job the digest equals the rank path's at any N."""
+    common = ["--host-walk", "--steps", "2", "--warmup", "1", "--global-packets", str(JOB)]
+    ranks = _line(_bench("--gpus", "2", *common))
+    for n in (1, 2, 8):
+        ip = _line(_bench("--gpus", str(n), "--in-process", *common))
+        assert ip["mode"] == "in-process" and ip["device_slots"] == n and not ip["valid_measurement"]
+        assert sum(s["packets_per_step"] for s in ip["per_slot"]) == JOB
+        assert ip["config"]["stats_digest"] == ranks["config"]["stats_digest"], n
+
+
+def test_bench_options_reach_the_context():
+    """--opt NAME=VALUE sets a per-context option on every context the bench creates; a bad one fails loudly."""
+    common = ["--host-walk", "--steps", "1", "--warmup", "0", "--global-packets", str(JOB)]
+    base = _line(_bench(*common))
+    forced = _line(_bench(*common, "--opt", "short_table=1", "--opt", "dt_parts=4"))
+    assert forced["config"]["stats_digest"] == base["config"]["stats_digest"]  # forms never change results
+    bad = _bench(*common, "--opt", "no_such_option=1")
+    assert bad.returncode != 0 and "unknown option" in bad.stderr
+
+
 def test_torchrun_world_size_must_match_gpus():
     p = _bench("--gpus", "3", "--host-walk", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "--gpus 3 but WORLD_SIZE=2" in p.stderr

@@ -35,28 +35,10 @@ def walk_vs_oracle(entries, tuples_from, n=20000, seed=1):
 
 @pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG0_DEMO, 0, 0), (W.CFG1_V4_10K, 0, 0), (W.CFG2_MIXED_1M, 100000, 512),
                                             (W.CFG4_ADVERSARIAL, 20000, 64)])
-def test_workloads_range_short_table(monkeypatch, cfg, npfx, ntmpl):
-    """The range form of the short table (INFW_SHORT_TABLE=dxr): the host walk equals the oracle."""
-    monkeypatch.setenv("INFW_SHORT_TABLE", "dxr")
+def test_workloads(cfg, npfx, ntmpl):
+    """The host walk of the compiled image equals the oracle."""
     wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
-    c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
-    assert c.info()["short_mode"] == 3 and c.info()["dxr_lines"] > 0
-
-
-@pytest.mark.parametrize("cfg,npfx,ntmpl,v6_form", [(W.CFG0_DEMO, 0, 0, ""), (W.CFG1_V4_10K, 0, 0, ""),
-                                                    (W.CFG2_MIXED_1M, 100000, 512, "std"),
-                                                    (W.CFG2_MIXED_1M, 100000, 512, "b2"),
-                                                    (W.CFG4_ADVERSARIAL, 20000, 64, "std"),
-                                                    (W.CFG4_ADVERSARIAL, 20000, 64, "b2")])
-def test_workloads(monkeypatch, cfg, npfx, ntmpl, v6_form):
-    """The host walk of the compiled image equals the oracle; IPv6 groups in either bucket form
-    (INFW_V6_FORM: one group per bucket, or the two-choice slot form)."""
-    if v6_form:
-        monkeypatch.setenv("INFW_V6_FORM", v6_form)
-    wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
-    c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
-    if v6_form:
-        assert (c.info()["v6_slot_buckets"] > 0) == (v6_form == "b2")
+    walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n))
 
 
 @pytest.mark.parametrize("cfg,npfx,ntmpl", [(W.CFG1_V4_10K, 0, 0), (W.CFG2_MIXED_1M, 100000, 512),
@@ -65,7 +47,7 @@ def test_workloads(monkeypatch, cfg, npfx, ntmpl, v6_form):
 def test_workloads_d16_words(monkeypatch, cfg, npfx, ntmpl, d16):
     """/16 words in front of DIR-24-8 forced off / on (INFW_D16): the host walk (which reads them like the
     kernel) equals the oracle either way."""
-    monkeypatch.setenv("INFW_D16", d16)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int(d16))
     wl = W.Workload(cfg, n_prefixes=npfx, n_templates=ntmpl)
     c, _ = walk_vs_oracle(list(wl.entries()), lambda n, s: wl.frames(s * n, n), n=30000)
     info = c.info()
@@ -76,7 +58,7 @@ def test_workloads_d16_words(monkeypatch, cfg, npfx, ntmpl, d16):
 def test_d16_chosen_for_sparse_short_tables(monkeypatch):
     """The automatic choice: configs[1] (10k /16../32 prefixes, one per /16 mostly) gets /16 words; a /16 packed
     with many BGP-like prefixes of several lists does not."""
-    monkeypatch.delenv("INFW_D16", raising=False)
+    monkeypatch.delitem(infw.DEFAULT_OPTIONS, "d16", raising=False)
     wl = W.Workload(W.CFG1_V4_10K)
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
     for k, v in wl.entries():
@@ -120,7 +102,7 @@ def test_distinct_lists_parallel_compile(monkeypatch):
     c, res = walk_vs_oracle(ents, lambda n, s: wl.frames(s * n, n), n=30000)
     info = c.info()
     assert info["n_lists"] >= 11900
-    monkeypatch.setenv("INFW_COMPILE_THREADS", "1")
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "compile_threads", int("1"))
     c1, res1 = walk_vs_oracle(ents, lambda n, s: wl.frames(s * n, n), n=30000)
     i1 = c1.info()
     for k in ("n_lists", "n_rules", "dt_parts", "n_tbl8_groups"):
@@ -192,9 +174,7 @@ def clustered_packets(anchors, n, seed):
     return hdr, cap, pl, np.array(ifx, np.uint32)
 
 
-@pytest.mark.parametrize("v6_form", ["std", "b2"])
-def test_clustered_overflow_groups(monkeypatch, v6_form):
-    monkeypatch.setenv("INFW_V6_FORM", v6_form)
+def test_clustered_overflow_groups():
     rng = random.Random(7)
     entries, anchors = _clustered_table(rng)
     c, res = walk_vs_oracle(entries, lambda n, seed: clustered_packets(anchors, n, seed), n=6000)
@@ -203,10 +183,8 @@ def test_clustered_overflow_groups(monkeypatch, v6_form):
     assert (res != 0).mean() > 0.3
 
 
-@pytest.mark.parametrize("v6_form", ["std", "b2"])
-def test_update_delete_churn_matches_oracle(monkeypatch, v6_form):
+def test_update_delete_churn_matches_oracle():
     """Random update/delete/commit churn: the compiled image tracks the map exactly."""
-    monkeypatch.setenv("INFW_V6_FORM", v6_form)
     rng = random.Random(11)
     entries, anchors = _clustered_table(rng, n_groups=15)
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
@@ -297,13 +275,9 @@ def test_host_sanitizer_walk():
     from conftest import run_make
     r = run_make("asan", timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
-    # the same harness with the IPv6 groups in the two-choice slot form (cuckoo placement, in-place patching)
-    env = dict(os.environ, INFW_V6_FORM="b2", ASAN_CHURN_ROUNDS="3")
-    r = subprocess.run([os.path.join(root, "ingress-node-firewall_amd", "build", "asan_walk")], cwd=root, env=env,
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
-    # and with /16 words in front of DIR-24-8 forced on (built per compile, re-derived by every patched commit)
-    env = dict(os.environ, INFW_D16="1", ASAN_CHURN_ROUNDS="3")
+    # the same harness with /16 words in front of DIR-24-8 forced on (built per compile, re-derived by every
+    # patched commit; the harness passes the option to the compiler)
+    env = dict(os.environ, ASAN_D16="1", ASAN_CHURN_ROUNDS="3")
     r = subprocess.run([os.path.join(root, "ingress-node-firewall_amd", "build", "asan_walk")], cwd=root, env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]

@@ -168,29 +168,24 @@ def test_partial_ifindex_prefixes():
     test_gpu_parity.py::test_partial_ifindex_prefixes_on_device."""
     entries, vals, hdr, cap, pl, fifx, tup = partial_ifindex_case()
     for mode in ("dir24", "compressed"):
-        import os
-        os.environ["INFW_SHORT_TABLE"] = mode
-        try:
-            c = infw.Classifier(flags=infw.F_HOST_ONLY)
-            m = orc.OracleMap()
-            for kb, rid in entries:
-                assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid])) == 0
-                assert m.update(kb, vals[rid]) == 0
-            c.commit()
-            want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
-            got = c.debug_walk(tup)
-            assert np.array_equal(got, want), mode
-            assert len({int(r) >> 8 for r in want}) >= 6  # defaults, own entries and unknown ifindexes all seen
-            assert [bytes(k) for k, _ in c.iterate()] == list(m.keys())
-            # delete the partial prefixes: the next commit (full) drops the defaults
-            for kb, rid in entries[5:]:
-                assert c.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb)) == m.delete(kb) == 0
-            c.commit()
-            assert c.info()["commit_mode"] == infw.COMMIT_FULL
-            want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
-            assert np.array_equal(c.debug_walk(tup), want), mode
-        finally:
-            del os.environ["INFW_SHORT_TABLE"]
+        c = infw.Classifier(flags=infw.F_HOST_ONLY, options={"short_table": {"dir24": 0, "compressed": 1}[mode]})
+        m = orc.OracleMap()
+        for kb, rid in entries:
+            assert c.update_rc(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid])) == 0
+            assert m.update(kb, vals[rid]) == 0
+        c.commit()
+        want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
+        got = c.debug_walk(tup)
+        assert np.array_equal(got, want), mode
+        assert len({int(r) >> 8 for r in want}) >= 6  # defaults, own entries and unknown ifindexes all seen
+        assert [bytes(k) for k, _ in c.iterate()] == list(m.keys())
+        # delete the partial prefixes: the next commit (full) drops the defaults
+        for kb, rid in entries[5:]:
+            assert c.delete_rc(infw.LpmIpKeySt.from_buffer_copy(kb)) == m.delete(kb) == 0
+        c.commit()
+        assert c.info()["commit_mode"] == infw.COMMIT_FULL
+        want, _, _, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
+        assert np.array_equal(c.debug_walk(tup), want), mode
 
 
 def test_ebpfsyncer_key_sets():

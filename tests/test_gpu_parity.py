@@ -18,6 +18,8 @@ from infw.batch import SoaBatch  # noqa: E402
 
 from parity import assert_parity, check_cfg, gpu_run, oracle_for, stats_from_results  # noqa: E402
 
+_SHORT = {"dir24": 0, "compressed": 1}  # option short_table (include/infw.h)
+
 
 @pytest.fixture(scope="module", autouse=True)
 def need_gpu():
@@ -53,12 +55,12 @@ def test_parity_dt_half_reads(monkeypatch, half):
     import orc
     from test_compiler_cpu import _val
     from test_incremental_cpu import _packets_for
-    monkeypatch.setenv("INFW_DT_HALF", half)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "dt_half", int(half))
     r = check_cfg(W.CFG1_V4_10K, 1 << 18)
     assert r["clf"].info()["dt_half_reads"] == int(half) and r["clf"].info()["d16"] == 1
     assert_parity(r, f"cfg1-dt-half{half}")
-    monkeypatch.setenv("INFW_D16", "1")
-    monkeypatch.setenv("INFW_DT_ADAPT", "0")
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int("1"))
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "dt_adapt", int("0"))
     for cfg, npfx, ntmpl in ((W.CFG2_MIXED_1M, 100000, 512), (W.CFG4_ADVERSARIAL, 20000, 64)):
         r = check_cfg(cfg, 1 << 18, npfx, ntmpl)
         assert r["clf"].info()["dt_half_reads"] == int(half) and r["clf"].info()["d16"] == 1
@@ -387,16 +389,12 @@ def test_partial_ifindex_prefixes_on_device():
     entries, vals, hdr, cap, pl, fifx, tup = partial_ifindex_case()
     dev = torch.device("cuda", 0)
     for mode in ("dir24", "compressed"):
-        os.environ["INFW_SHORT_TABLE"] = mode
-        try:
-            c = infw.Classifier(devices=[0])
-            m = orc.OracleMap()
-            for kb, rid in entries:
-                c.update(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid]))
-                m.update(kb, vals[rid])
-            c.commit()
-        finally:
-            del os.environ["INFW_SHORT_TABLE"]
+        c = infw.Classifier(devices=[0], options={"short_table": _SHORT[mode]})
+        m = orc.OracleMap()
+        for kb, rid in entries:
+            c.update(infw.LpmIpKeySt.from_buffer_copy(kb), infw.RulesValSt.from_buffer_copy(vals[rid]))
+            m.update(kb, vals[rid])
+        c.commit()
         gres, gver = gpu_run(c, SoaBatch.from_tuples(tup, dev), tup.shape[0])
         want, over, ost, _ = m.classify_frames(hdr, cap, pl, fifx, nthreads=2)
         assert np.array_equal(gres, want), mode
@@ -421,35 +419,12 @@ def test_device_frame_generator():
     assert np.array_equal(ifx.cpu().numpy().view(np.uint32), fx)
 
 
-def test_parity_v6_slot_form(monkeypatch):
-    """The opt-in two-choice slot form of the IPv6 groups (INFW_V6_FORM=b2: two groups per 64-B bucket, cuckoo
-    placement, second-bucket reads behind the DISPLACED flag) classifies bit-identically — configs[2] (one-record
-    groups) and configs[4] (two-record groups taking a whole bucket, > 2 records in the Waldvogel table)."""
-    monkeypatch.setenv("INFW_V6_FORM", "b2")
-    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
-    assert_parity(r, "cfg2-v6-slots")
-    r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 0, 0)
-    assert_parity(r, "cfg4-v6-slots")
-
-
-def test_parity_range_short_table(monkeypatch):
-    """The range form of the <= /32 key space (INFW_SHORT_TABLE=dxr: per /16 chunk one answer or one line of
-    <= 11 runs) classifies bit-identically on configs[1], [2] (100k prefixes) and [4]."""
-    monkeypatch.setenv("INFW_SHORT_TABLE", "dxr")
-    r = check_cfg(W.CFG1_V4_10K, 1 << 18)
-    assert_parity(r, "cfg1-dxr")
-    r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
-    assert_parity(r, "cfg2-dxr")
-    r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64)
-    assert_parity(r, "cfg4-dxr")
-
-
 @pytest.mark.parametrize("d16", ["0", "1"])
 def test_parity_d16_words(monkeypatch, d16):
     """/16 words in front of DIR-24-8 (infw_tables.h; INFW_D16 forces them on or off, the compiler chooses them
     for sparse short tables such as configs[1] and [4]): bit-identical either way, on configs[1], [2] (100k
     prefixes, and the full 1M table, where the compiler would not choose them) and [4]."""
-    monkeypatch.setenv("INFW_D16", d16)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int(d16))
     for cfg, n, npfx, ntmpl, start in [(W.CFG1_V4_10K, 1 << 18, 0, 0, 0), (W.CFG2_MIXED_1M, 1 << 18, 100000, 512, 0),
                                        (W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64, 0),
                                        (W.CFG2_MIXED_1M, 1 << 17, 0, 0, (1 << 26) + 777)]:
@@ -460,7 +435,7 @@ def test_parity_d16_words(monkeypatch, d16):
 def test_parity_compressed_short_table(monkeypatch):
     """The compressed 16-8-8 short-table form (chosen automatically when DIR-24-8 would exceed its memory
     budget, e.g. many ifindexes) classifies bit-identically."""
-    monkeypatch.setenv("INFW_SHORT_TABLE", "compressed")
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "short_table", _SHORT["compressed"])
     r = check_cfg(W.CFG2_MIXED_1M, 1 << 18, 100000, 512)
     assert_parity(r, "cfg2-compressed")
     r = check_cfg(W.CFG4_ADVERSARIAL, 1 << 18, 20000, 64)
@@ -538,20 +513,17 @@ def _frames_run(clf, dbuf, lens, fifx, n, dev, plen=None, offs=None, stride=0):
     return res.cpu().numpy().view(np.uint32)[:n], ver.cpu().numpy()[:n], clf.stats_read_all()
 
 
-@pytest.mark.parametrize("short_table,v6_form,d16", [("dir24", "std", "1"), ("dir24", "std", "0"), ("compressed", "std", ""),
-                                                    ("dxr", "b2", "")])
-def test_classify_frames_on_device(monkeypatch, short_table, v6_form, d16):
+@pytest.mark.parametrize("short_table,d16", [("dir24", "1"), ("dir24", "0"), ("compressed", "")])
+def test_classify_frames_on_device(monkeypatch, short_table, d16):
     """§8f-3 classification straight from raw frames (infw_classify_frames: the tuple is built in the kernel from
     the staged header window): result words, verdicts and counters equal the oracle's on the same frames —
     header snapshots at a fixed stride (a ragged count), and variable-length real frames back to back with an
     offset array (truncated ones, the shortest at the very end of the buffer).  The compressed short table runs
-    the kernel's full (non-lean) instantiation; the range short table with the IPv6 slot form covers the opt-in
-    table forms in the frames kernel."""
+    the kernel's full (non-lean) instantiation."""
     from frames import frame, snapshots
-    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
-    monkeypatch.setenv("INFW_V6_FORM", v6_form)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "short_table", _SHORT[short_table])
     if d16:  # /16 words in front of DIR-24-8 forced on / off
-        monkeypatch.setenv("INFW_D16", d16)
+        monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int(d16))
     dev = torch.device("cuda", 0)
     for cfg, npre, ntpl in ((W.CFG2_MIXED_1M, 50000, 256), (W.CFG4_ADVERSARIAL, 20000, 64)):
         wl = W.Workload(cfg, n_prefixes=npre, n_templates=ntpl)
@@ -664,7 +636,7 @@ def test_survey_probes_on_device(monkeypatch, short_table):
     import goenc
     from frames import snapshots
     from test_golden import expected_stats, load, probe_frames
-    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "short_table", _SHORT[short_table])
     dev = torch.device("cuda", 0)
     for case in load("survey_probes.json")["cases"]:
         c = infw.Classifier(devices=[0])
@@ -832,9 +804,9 @@ def test_incremental_commits_on_device(monkeypatch, d16, split):
     import orc
     from test_incremental_cpu import _apply, _packets_for, _val
     if d16:
-        monkeypatch.setenv("INFW_D16", d16)
+        monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int(d16))
     if split:
-        monkeypatch.setenv("INFW_SPLIT", split)
+        monkeypatch.setitem(infw.DEFAULT_OPTIONS, "split", int(split))
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=100000, n_templates=512)
     ents = list(wl.entries())
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 4096)
@@ -1082,7 +1054,7 @@ def test_lds_d16_cache_collisions(monkeypatch):
     import orc
     import goenc
     from test_incremental_cpu import _packets_for
-    monkeypatch.setenv("INFW_D16", "1")
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "d16", int("1"))
     rng = random.Random(12)
     idx_bits = 10  # the per-list-part-count shape: 2048 LDS words = 1024 /16-word entries
     his = []
@@ -1121,7 +1093,7 @@ def test_classify_host_batches(monkeypatch, split):
     pageable and page-locked memory) gives the same result words, verdicts and counters as the oracle — also in
     the two-phase form, whose per-chunk scratch is allocated on the pipeline's kernel stream."""
     if split:
-        monkeypatch.setenv("INFW_SPLIT", split)
+        monkeypatch.setitem(infw.DEFAULT_OPTIONS, "split", int(split))
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
@@ -1182,7 +1154,7 @@ def test_counter_paths(monkeypatch, flush_tiles):
     words: workgroups flushing after every tile / every 3 tiles / at the default interval, and 1 % of the frames
     with lengths of 2^20 B or more (up to 2^32 - 1), which bypass the packed counters."""
     if flush_tiles:
-        monkeypatch.setenv("INFW_STAT_FLUSH_TILES", flush_tiles)
+        monkeypatch.setitem(infw.DEFAULT_OPTIONS, "stat_flush_tiles", int(flush_tiles))
     wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
     clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
     wl.load_into(clf)
@@ -1205,8 +1177,8 @@ def test_counter_paths(monkeypatch, flush_tiles):
     assert int(want[:, 1].max()) > (1 << 32) or int(want[:, 3].max()) > (1 << 32)  # byte sums past 32 bits
 
 
-@pytest.mark.parametrize("v6_form,short_table", [("std", "dir24"), ("b2", "dir24"), ("std", "compressed")])
-def test_clustered_adversarial_tables_on_device(monkeypatch, v6_form, short_table):
+@pytest.mark.parametrize("short_table", ["dir24", "compressed"])
+def test_clustered_adversarial_tables_on_device(monkeypatch, short_table):
     """Every LPM corner on the device (tests/test_compiler_cpu.py `_clustered_table`): IPv6 prefixes clustered
     under few /32s (groups past 3 records: the Waldvogel overflow table, the non-lean kernel), nested lengths
     /0../128 on three ifindexes (one above 2^16), IPv4 nesting, cross-family aliases; rule values with rule ids 0,
@@ -1215,8 +1187,7 @@ def test_clustered_adversarial_tables_on_device(monkeypatch, v6_form, short_tabl
     import random
     import orc
     from test_compiler_cpu import _clustered_table, clustered_packets
-    monkeypatch.setenv("INFW_V6_FORM", v6_form)
-    monkeypatch.setenv("INFW_SHORT_TABLE", short_table)
+    monkeypatch.setitem(infw.DEFAULT_OPTIONS, "short_table", _SHORT[short_table])
     entries, anchors = _clustered_table(random.Random(7))
     clf = infw.Classifier(devices=[0])
     m = orc.OracleMap()

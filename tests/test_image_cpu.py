@@ -128,10 +128,10 @@ HDR = 72  # magic 8, format 4, abi 4, build id 32, element sizes 16, payload XXH
 # (name, kind, element size) in image.cpp's order: the entry set, tables_io(), tbl8_of, then the IncState
 _TABLES = [("if_keys", "v", 4), ("if_slot", "v", 4), ("if_mult", "p", 4), ("if_shift", "p", 4), ("n_slots", "p", 4),
            ("l16", "v", 4), ("nodes", "v", 64), ("vpool", "v", 4), ("n_tbl8_groups", "p", 8), ("tbl24", "v", 8),
-           ("tbl8", "v", 4), ("d24_inline", "p", 1), ("short_mode", "p", 4), ("ltab", "v", 32), ("btab", "v", 64),
-           ("n_buckets", "p", 8), ("n_overflow_groups", "p", 8), ("b2n", "p", 8), ("wild", "v", 4), ("n_wild", "p", 4),
+           ("tbl8", "v", 4), ("short_mode", "p", 4), ("ltab", "v", 32), ("btab", "v", 64),
+           ("n_buckets", "p", 8), ("n_overflow_groups", "p", 8), ("wild", "v", 4), ("n_wild", "p", 4),
            ("levels", "v", 1), ("desc", "v", 8), ("rules", "v", 8), ("dte", "v", 64), ("dtl", "v", 64),
-           ("dt_plog2", "p", 4), ("dt_pl", "v", 4), ("dxr_idx", "v", 4), ("dxr_lines", "v", 64), ("d16", "v", 8),
+           ("dt_plog2", "p", 4), ("dt_pl", "v", 4), ("d16", "v", 8),
            ("d16_on", "p", 4), ("d16_permille", "p", 4), ("dt_half", "p", 4), ("n_lists", "p", 4), ("n_entries", "p", 8),
            ("n_long_entries", "p", 8)]
 
@@ -323,6 +323,73 @@ def test_import_into_emptied_context():
     b.commit()
     b.import_image(img)
     assert b.export_image() == img and b.count() == a.count()
+
+
+def _dup_values_image(img: bytes) -> bytes:
+    """The image with its second interned value overwritten by its first (a valid hash): the entry set then names
+    two equal values, which the importer must refuse before it touches the map."""
+    b = bytearray(img)
+    secs = image_sections(img)
+    off, n = secs["values"]
+    assert n >= 2400
+    b[off + 1200:off + 2400] = b[off:off + 1200]
+    return rehash(b)
+
+
+def test_refused_import_changes_nothing():
+    """a refused import leaves the context as it was.
+    - A populated context with committed entries and uncommitted edits: busy is decided before the image is read,
+      so a corrupt image gets -EBUSY too and the pending edits survive; they commit and walk like the oracle.
+    - An emptied context (its entries removed and committed; its compiled lists still map value ids): imports
+      refused for too many entries (-ENOSPC), a torn payload and duplicate values (-EINVAL) keep its value pool, so
+      the next update + incremental commit classifies with the new value's own rules, as the oracle does."""
+    wl, a = _wl_ctx(W.CFG1_V4_10K, 2000, 16)
+    img = a.export_image()
+    torn = bytearray(img)
+    torn[len(torn) // 2] ^= 1
+    rng = random.Random(3)
+    vals = [bytes(v) for _, v in wl.entries()][:64]
+    v1 = next(v for v in vals if v != vals[0])
+    # populated
+    b = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=4096)
+    m = orc.OracleMap()
+    keys = [bytes(infw.build_ebpf_key(3, f"10.{i}.0.0/16")) for i in range(8)]
+    for k in keys[:4]:
+        _apply([b], m, k, vals[0])
+    b.commit()
+    for k in keys[4:]:
+        _apply([b], m, k, v1)  # uncommitted
+    for bad in (img, bytes(torn), _dup_values_image(img)):
+        with pytest.raises(infw.InfwError) as e:
+            b.import_image(bad)
+        assert e.value.errno == 16
+        assert b.count() == 8
+    b.commit()
+    hdr, cap, pl, ifx = _packets_for(keys, rng)
+    tup = W.pack_frames(hdr, cap, pl, ifx)
+    want, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
+    assert np.array_equal(b.debug_walk(tup), want)
+    # emptied
+    for bad, errno in ((img, 28), (bytes(torn), 22), (_dup_values_image(img), 22)):
+        e_ctx = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=16 if errno == 28 else 4096)
+        m = orc.OracleMap()
+        k0, k1 = keys[0], keys[1]
+        _apply([e_ctx], m, k0, vals[0])
+        e_ctx.commit()
+        _apply([e_ctx], m, k0, None)
+        e_ctx.commit()
+        with pytest.raises(infw.InfwError) as e:
+            e_ctx.import_image(bad)
+        assert e.value.errno == errno, N.last_error()
+        assert e_ctx.count() == 0
+        _apply([e_ctx], m, k1, v1)
+        e_ctx.commit()
+        assert e_ctx.info()["commit_mode"] == infw.COMMIT_INCREMENTAL
+        hdr, cap, pl, ifx = _packets_for([k0, k1], rng, per_key=300)
+        tup = W.pack_frames(hdr, cap, pl, ifx)
+        want, _, _, _ = m.classify_frames(hdr, cap, pl, ifx)
+        assert np.array_equal(e_ctx.debug_walk(tup), want), errno
+        assert (want != 0).any()
 
 
 ASAN_ABI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ingress-node-firewall_amd",

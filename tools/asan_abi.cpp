@@ -265,9 +265,8 @@ static int selftest() {
         std::vector<uint32_t> vi(keys.size());
         for (auto &x : vi) x = rnd() % vals.size();
         CHECK(infw_table_update_batch(s.c, keys.data(), vals.data(), vi.data(), keys.size(), 0, nullptr) == 0);
-        setenv("INFW_SHORT_TABLE", "compressed", 1);
+        CHECK(infw_set_option(s.c, "short_table", 1) == 0);
         const int rc = infw_table_commit(s.c);
-        unsetenv("INFW_SHORT_TABLE");
         CHECK(rc == 0 && infw_table_info(s.c, &info) == 0 && info.short_mode == 1);
         if (export_image(s.c, small_img)) return 1;
     }
@@ -295,6 +294,26 @@ static int selftest() {
         std::vector<uint8_t> img_d;
         if (export_image(d.c, img_d)) return 1;
         CHECK(img_d == img);
+    }
+    // options: unknown names and out-of-range values are refused and change nothing; every listed option reads back
+    {
+        Ctx o(1u << 10);
+        int64_t v = 0;
+        CHECK(infw_set_option(o.c, "no_such_option", 1) == -EINVAL);
+        CHECK(infw_set_option(o.c, nullptr, 1) == -EINVAL);
+        CHECK(infw_set_option(o.c, "dt_parts", 3) == -EINVAL);
+        CHECK(infw_set_option(o.c, "split", 2) == -EINVAL);
+        CHECK(infw_set_option(o.c, "stat_flush_tiles", 0) == -EINVAL);
+        CHECK(infw_get_option(o.c, "split", &v) == 0 && v == -1);
+        CHECK(infw_get_option(o.c, "stat_flush_tiles", &v) == 0 && v == 1024);
+        CHECK(infw_set_option(o.c, "dt_parts", 8) == 0 && infw_get_option(o.c, "dt_parts", &v) == 0 && v == 8);
+        int n_opt = 0;
+        for (; infw_option_name(n_opt); n_opt++) CHECK(infw_get_option(o.c, infw_option_name(n_opt), &v) == 0);
+        CHECK(n_opt == 11);
+        char name[256];
+        CHECK(infw_classify_variant(o.c, 0, INFW_INPUT_SOA, 0, name, sizeof name) == 0);
+        CHECK(infw_classify_variant(o.c, 0, INFW_INPUT_SOA, 0, name, 4) == -ERANGE);
+        CHECK(infw_classify_variant(o.c, 0, 7, 0, name, sizeof name) == -EINVAL);
     }
     printf("asan_abi: %zu keys, images %zu / %zu bytes, %zu corrupt images refused\nok\n", keys.size(), img.size(),
            small_img.size(), refused);

@@ -41,6 +41,15 @@ static void random_value(uint8_t *val, int n_rules) {
     }
 }
 
+// The compiler options of this harness: the short-table form asked for, /16 words per ASAN_D16 (the harness's own
+// switch; the library reads no environment).
+static Options opts(int mode) {
+    Options o;
+    o.short_table = mode == (int)INFW_SHORT_COMPRESSED ? 1 : mode == (int)INFW_SHORT_DIR24 ? 0 : -1;
+    if (const char *e = getenv("ASAN_D16")) o.d16 = atoi(e);
+    return o;
+}
+
 static int run_case(int n_keys, int v4_share, int max_rules, int mode, int seed) {
     rs = 0x9E3779B97F4A7C15ull * (uint64_t)(seed + 1);
     PendingMap m;
@@ -59,7 +68,7 @@ static int run_case(int n_keys, int v4_share, int max_rules, int mode, int seed)
         m.update(&k, val, 0);
     }
     HostTables h;
-    int rc = compile_tables(m, h, mode, mode < 0 ? 0 : (4ull << 30));
+    int rc = compile_tables(m, h, opts(mode));
     if (rc) return rc;
     const infw_dev_tables t = h.view();
     uint64_t hits = 0;
@@ -116,7 +125,7 @@ static int run_churn(int n_keys, int seed) {
     }
     HostTables h;
     IncState inc;
-    if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
+    if (compile_tables(m, h, opts(INFW_SHORT_DIR24), &inc)) return -1;
     m.clear_dirty();
     int patched = 0, full = 0;
     const int rounds = getenv("ASAN_CHURN_ROUNDS") ? atoi(getenv("ASAN_CHURN_ROUNDS")) : 8;
@@ -137,12 +146,12 @@ static int run_churn(int n_keys, int seed) {
         }
         std::vector<DirtyRange> ranges;
         std::string why;
-        int rc = patch_tables(m, h, inc, ranges, &why);
+        int rc = patch_tables(m, h, inc, ranges, &why, opts(INFW_SHORT_DIR24));
         if (rc != 0) {  // a layout change: recompile, as infw_table_commit does
             full++;
             h = HostTables();
             inc = IncState();
-            if (compile_tables(m, h, INFW_SHORT_DIR24, 4ull << 30, &inc)) return -1;
+            if (compile_tables(m, h, opts(INFW_SHORT_DIR24), &inc)) return -1;
         } else {
             patched++;
             for (const DirtyRange &d : ranges) {
@@ -158,7 +167,7 @@ static int run_churn(int n_keys, int seed) {
         }
         m.clear_dirty();
         HostTables f;
-        if (compile_tables(m, f, INFW_SHORT_DIR24, 4ull << 30)) return -1;
+        if (compile_tables(m, f, opts(INFW_SHORT_DIR24))) return -1;
         const infw_dev_tables tp = h.view(), tf = f.view();
         for (int i = 0; i < 20000; i++) {
             uint32_t sa[4] = {rnd(), rnd(), rnd(), rnd()};

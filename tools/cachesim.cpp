@@ -134,7 +134,7 @@ int main(int argc, char **argv) {
     const rulesVal_st *tv = infw_wl_templates(wl);
     for (uint64_t i = 0; i < ne; i++) m.update(&keys[i], reinterpret_cast<const uint8_t *>(&tv[vi[i]]), 0);
     HostTables h;
-    if (compile_tables(m, h, 0)) return 2;
+    if (compile_tables(m, h, Options())) return 2;
     const infw_dev_tables t = h.view();
     std::vector<uint32_t> tup(n * 8);
     infw_wl_tuples(wl, 0, n, tup.data(), 8);

@@ -10,7 +10,7 @@
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
-#   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: split split2 split3 split4 d16cache cfg1_shape)
+#   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: keyorder split fstride)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
 set -u
 TAG=${1:?tag}; shift

@@ -39,7 +39,7 @@ int main(int argc, char **argv) {
     HostTables h;
     IncState inc;
     auto t = std::chrono::steady_clock::now();
-    if (compile_tables(m, h, -1, 4ull << 30, &inc)) return 1;
+    if (compile_tables(m, h, Options(), &inc)) return 1;
     printf("cfg%d: %zu entries, compile %.0f ms\n", cfg, m.nodes.size(), ms_since(t));
     m.clear_dirty();
     std::mt19937_64 rng(7);
@@ -87,14 +87,16 @@ int main(int argc, char **argv) {
         std::vector<DirtyRange> ranges;
         std::string why;
         t = std::chrono::steady_clock::now();
-        const int rc = patch_tables(m, h, inc, ranges, &why);
+        Options po;
+        if (getenv("PB_TRACE")) po.trace = 2;  // the patch's per-phase trace (option trace, bit 2)
+        const int rc = patch_tables(m, h, inc, ranges, &why, po);
         pat.push_back(ms_since(t));
         if (rc == 1) {  // the edit needs a full compile (counted apart)
             printf("round %d: full compile (%s)\n", r, why.c_str());
             pat.pop_back();
             h = HostTables();
             inc = IncState();
-            if (compile_tables(m, h, -1, 4ull << 30, &inc)) return 1;
+            if (compile_tables(m, h, Options(), &inc)) return 1;
         } else if (rc) {
             printf("round %d: patch rc %d\n", r, rc);
             return 1;
