@@ -829,7 +829,8 @@ def run_in_process(args, n_slots):
                    "rule_lists": info["n_lists"], "global_batch": job,
                    "parallelism": f"{n_slots} device slot(s) of one context on device(s) {sorted(set(devices))}, "
                                   "one host thread + stream each, counters summed per rule over slots",
-                   "packets_counted_in_stats": int(digest_block[:, 0].sum() + digest_block[:, 2].sum()),
+                   # over the timed steps, as the rank path counts them
+                   "packets_counted_in_stats": int(total[:, 0].sum() + total[:, 2].sum()),
                    "stats_digest": stats_digest(digest_block),
                    "tables": {"setup_s": round(setup_s, 2), "device_ms_max": round(info["device_ms_max"], 1),
                               "n_device_slots": info["n_device_slots"]}},

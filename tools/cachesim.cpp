@@ -132,7 +132,31 @@ int main(int argc, char **argv) {
     const lpm_ip_key_st *keys = infw_wl_keys(wl);
     const uint32_t *vi = infw_wl_val_index(wl);
     const rulesVal_st *tv = infw_wl_templates(wl);
-    for (uint64_t i = 0; i < ne; i++) m.update(&keys[i], reinterpret_cast<const uint8_t *>(&tv[vi[i]]), 0);
+    // CACHESIM_SHUFFLE=1: the keys in a seeded random order, as bench.py's default --key-order shuffled (the
+    // reference loader's Go map range): the last update of every entry, shuffled — the same map, other list ids
+    std::vector<uint64_t> order(ne);
+    for (uint64_t i = 0; i < ne; i++) order[i] = i;
+    if (getenv("CACHESIM_SHUFFLE") && atoi(getenv("CACHESIM_SHUFFLE"))) {
+        std::unordered_map<std::string, uint64_t> last;
+        for (uint64_t i = 0; i < ne; i++) {
+            NodeKey k;
+            k.plen = keys[i].prefixLen;
+            uint8_t md[20];
+            memcpy(md, &keys[i].ingress_ifindex, 4);
+            memcpy(md + 4, keys[i].ip_data, 16);
+            mask_bits(md, k.plen, k.md, 20);
+            last[std::string(reinterpret_cast<const char *>(&k), sizeof k)] = i;
+        }
+        order.clear();
+        for (const auto &kv : last) order.push_back(kv.second);
+        std::sort(order.begin(), order.end());
+        uint64_t rs = 0x5EED;
+        for (uint64_t i = order.size(); i > 1; i--) {  // Fisher-Yates with a fixed-seed generator
+            rs = rs * 6364136223846793005ull + 1442695040888963407ull;
+            std::swap(order[i - 1], order[(rs >> 33) % i]);
+        }
+    }
+    for (uint64_t i : order) m.update(&keys[i], reinterpret_cast<const uint8_t *>(&tv[vi[i]]), 0);
     HostTables h;
     if (compile_tables(m, h, Options())) return 2;
     const infw_dev_tables t = h.view();
