@@ -621,6 +621,9 @@ def run_rank(args):
                 if rates:  # the fabric's line traffic against the stream bandwidth this process measured
                     extra["line_traffic_frac_of_stream"] = round(extra["line_traffic_GBps_at_128B"] /
                                                                  rates["stream_GB_per_s"], 3)
+                    # the one bound the line counts give: at this build's lines per packet the kernel can run at
+                    # most this much faster before its 128-B lines fill the measured stream bandwidth
+                    extra["headroom_at_current_lines"] = round(1.0 / max(extra["line_traffic_frac_of_stream"], 1e-9), 3)
                 extra["fetch_size_GBps"] = round(traffic / (avg_kern_ms * 1e-3) / 1e9, 1) if traffic else None
             if "lds_bank_conflict_rate" in tj:
                 extra["lds_bank_conflict_rate"] = round(tj["lds_bank_conflict_rate"], 4)
