@@ -7,7 +7,8 @@
 #   keyorder   configs[2]: the reference loader's random update order (default) vs the generator's popularity order
 #              (--key-order workload: hot rule lists get adjacent ids, so their decision lines sit together)
 #   split      configs[2] with one rule list per key: fused vs the two-phase form (option split)
-#   fstride    classification straight from frames (--fused) at frame strides 64 / 128 / 256 B
+#   fstride    classification straight from frames (--fused) at frame strides 80 (header snapshots back to back: the
+#              window of every other frame straddles two 64-B sectors) / 128 / 256 / 512 B
 set -u
 TAG=${1:?tag}; EXP=${2:?experiment}
 O=gpurun_out/$TAG/ab_$EXP
@@ -31,9 +32,10 @@ arms() {  # one round of the experiment's arms
       run fused_$1 --opt split=0
       run split_$1 --opt split=1 ;;
     fstride)
-      run s64_$1 --from-frames 64 --fused
+      run s80_$1 --from-frames 80 --fused
       run s128_$1 --from-frames 128 --fused
-      run s256_$1 --from-frames 256 --fused ;;
+      run s256_$1 --from-frames 256 --fused
+      run s512_$1 --from-frames 512 --fused ;;
     *) echo "unknown experiment $EXP" >&2; exit 2 ;;
   esac
 }
