@@ -179,10 +179,19 @@ def parse(argv=None):
                     help="with --in-process: every slot on device 0 (rehearsal of the N-slot shape on one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="per-context option (include/infw.h) for every context this bench creates")
+    ap.add_argument("--xdp-ring", choices=("hbm", "host"), default=None,
+                    help="AF_XDP feed: the frames in a umem of 2048-B chunks (--from-frames sets another chunk size) "
+                         "in HBM or pinned host memory (read over PCIe), one RX descriptor ring per interface, "
+                         "classified by infw_classify_xdp (implies --fused)")
     ap.add_argument("--fused", action="store_true",
                     help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
                          "no SoA batch written or read; checked untimed against the packer path's results")
     args = ap.parse_args(argv)
+    if args.xdp_ring:
+        args.from_frames = args.from_frames or 2048
+        args.fused = True
+        if args.batch == 1 << 27:
+            args.batch = 1 << 24  # 16M frames x 2048 B = 32 GiB of umem
     args.options = {}
     for o in args.opt:
         name, _, val = o.partition("=")
@@ -477,6 +486,48 @@ def run_rank(args):
             clf.stats_reset()
         args.layout = "frames"
         algo_bytes = 27 + 12 * n6 / max(n, 1)  # frame bytes kernel.c reads (11 B IPv4, 23 B IPv6) + 12 B lengths/ifindex + result
+    rings, perm = [], None
+    if args.xdp_ring and n:
+        # one AF_XDP RX ring per interface (a socket is bound to one interface queue): descriptor {addr, len} of
+        # every frame of that interface, in arrival order; len = the frame's linear length when its linear part ends
+        # inside the 80-B snapshot, else its frame length (single-buffer frames)
+        ifx_h = f_ifx[:n].cpu().numpy().view(np.uint32)
+        lin_h = f_lin[:n].cpu().numpy().view(np.uint32)
+        len_h = np.where(lin_h < 80, lin_h, f_len[:n].cpu().numpy().view(np.uint32))
+        order = []
+        for ifv in np.unique(ifx_h):
+            idx = np.nonzero(ifx_h == ifv)[0]
+            d = np.zeros((len(idx), 4), np.uint32)
+            a = idx.astype(np.uint64) * np.uint64(stride)
+            d[:, 0], d[:, 1], d[:, 2] = a & np.uint64(0xFFFFFFFF), a >> np.uint64(32), len_h[idx]
+            rings.append([int(ifv), len(idx), torch.from_numpy(d.view(np.int32))])
+            order.append(idx)
+        perm = torch.from_numpy(np.concatenate(order)).to(dev)
+        if args.xdp_ring == "host":  # umem and rings in pinned host memory: the kernel reads them over PCIe
+            umem = torch.empty(frames.numel(), dtype=torch.uint8, pin_memory=True)
+            umem.copy_(frames)
+            del frames
+            frames = umem
+            for r in rings:
+                r[2] = r[2].pin_memory()
+        else:
+            for r in rings:
+                r[2] = r[2].to(dev)
+        algo_bytes = 11 + 12 * n6 / max(n, 1) + 16 + 4  # frame bytes read + the 16-B descriptor + the result word
+        # untimed: the rings' result words, back in packet order, == the packer path's (counters: the digest below)
+        ref = torch.empty_like(results)
+        clf.classify_c(batch_c, results=ref)
+        off = 0
+        for ifv, nr, d in rings:
+            clf.classify_xdp(frames, d, nr, ifv, results=results[off:off + nr])
+            off += nr
+        got = torch.empty_like(results)
+        got[perm] = results
+        torch.cuda.synchronize()
+        fused_check = bool(torch.equal(ref, got))
+        assert fused_check, "classify_xdp differs from pack_frames_c + classify_c"
+        del ref, got
+        clf.stats_reset()
     ex = StatsExchange(lambda: torch.zeros((1024, 4), dtype=torch.int64, device=dev), use_dist)
     # the device's random-line and stream rates, measured in this process just before the timed loop (same lease,
     # same device): what random_line_model prices the kernel's PMC line counts with (~0.3 s, untimed)
@@ -489,7 +540,14 @@ def run_rank(args):
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
-        if args.fused:
+        if args.xdp_ring:
+            if ev is not None:
+                ev[2].record(stream)
+            off = 0
+            for ifv, nr, d in rings:  # one launch per interface ring
+                clf.classify_xdp(frames, d, nr, ifv, results=results[off:off + nr], stream=stream)
+                off += nr
+        elif args.fused:
             if ev is not None:
                 ev[2].record(stream)
             clf.classify_frames(frames, f_lin[:n], f_ifx[:n], n, results=results, pkt_len=f_len[:n], stride=stride,
@@ -556,7 +614,14 @@ def run_rank(args):
     # the registry name of the instantiation(s) this line ran (infw_classify_variant: the library's own selector)
     kernel = clf.variant({"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
                           "frames": infw.INPUT_FRAMES}[args.layout])
-    if args.fused:
+    if args.xdp_ring:
+        extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "chunk": stride, "rings": len(rings),
+                                   "frames_per_ring": [r[1] for r in rings],
+                                   "results_equal_packer_path": fused_check,
+                                   "note": "umem and descriptor rings in " + (
+                                       "pinned host memory, read by the kernel over PCIe (PCIe-inclusive rate)"
+                                       if args.xdp_ring == "host" else "HBM")}}
+    elif args.fused:
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,
                                       "results_equal_packer_path": fused_check}}
     elif args.from_frames:
@@ -575,6 +640,7 @@ def run_rank(args):
         extra_pipe = {}
     wkey = workload_key(args.cfg, args.templates, args.prefixes) + ("_uniform" if args.uniform else "") + (
         "_frames" if args.from_frames else "") + ("_fused" if args.fused else "") + (
+        f"_xdp{args.xdp_ring}" if args.xdp_ring else "") + (
         "_compact" if args.layout == "compact" and not args.from_frames else "")
 
     traffic = None
@@ -696,6 +762,10 @@ def run_rank(args):
 
     # ---- CPU baseline: the oracle (plain C restatement of kernel.c) on host cores, rank 0, N=1 only
     if world == 1 and rank == 0 and not args.no_cpu_baseline and n:
+        if perm is not None:  # the rings' results back into packet order
+            in_order = torch.empty_like(results)
+            in_order[perm] = results
+            results = in_order
         out["cpu_baseline"] = cpu_baseline(args, wl, results, n, start)
 
     if rank == 0:

@@ -342,6 +342,27 @@ int infw_pack_frames_c(infw_ctx *ctx, int dev, const struct infw_frame_batch *fr
 int infw_classify_frames(infw_ctx *ctx, int dev, const struct infw_frame_batch *frames, uint64_t n,
                          uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
 
+/* An AF_XDP socket's RX ring as the feed (the NIC side of   */
+/* the frames path): descriptors as the kernel writes them into the ring      */
+/* (linux/if_xdp.h struct xdp_desc), frames in the socket's umem.  Frame i's  */
+/* bytes start at umem + (addr & (2^48 - 1)) + (addr >> 48) — aligned mode,    */
+/* and unaligned mode's offset in bits 48..63 (XSK_UNALIGNED_BUF_OFFSET_SHIFT) */
+/* — and len is both its linear length (xdp data .. data_end) and             */
+/* bpf_xdp_get_buff_len(): single-buffer frames (a multi-buffer frame's first */
+/* descriptor is classified on its own bytes and length).  One ring belongs  */
+/* to one interface queue, so every frame carries `ifindex`.  umem and descs  */
+/* must be device-accessible: HBM, or pinned host memory (hipHostMalloc), which */
+/* the kernel reads in place over PCIe — one 64-B header window and one 16-B  */
+/* descriptor per frame.  descs 16-byte aligned.  Identical results and       */
+/* counters to infw_classify_frames over the same frames.  Asynchronous.      */
+struct infw_xdp_desc {
+    uint64_t addr;
+    uint32_t len;
+    uint32_t options;
+};
+int infw_classify_xdp(infw_ctx *ctx, int dev, const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n,
+                      uint32_t ifindex, uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */
 /*  - Deny events (kernel.c:392-399, ingress_node_firewall_events_map): one  */

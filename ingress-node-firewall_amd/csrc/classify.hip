@@ -298,6 +298,10 @@ struct BatchIn {
     const uint64_t *offsets;
     uint64_t fstride;
     const uint32_t *linear_len;
+    // or AF_XDP RX descriptors (infw_classify_xdp): {addr, len, options} per frame into `frames` (the umem), one
+    // ifindex for the ring; addr's bits 48..63 carry the unaligned-mode offset (XSK_UNALIGNED_BUF_OFFSET_SHIFT)
+    const u32x4 *xdp;
+    uint32_t xdp_ifindex;
     // kSplit (the two-phase form): phase 1 writes one word per packet here (split_word), phase 2 reads it
     uint64_t *mid;
 };
@@ -546,7 +550,16 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa,
                           bool with_meta = true) {
         if (kF) {  // frames: linear length (meta), frame byte offset (sa.x/sa.y), ifindex, frame length
-            if (i < n) {
+            if (i < n && in.xdp) {  // one 16-B descriptor per frame (a uniform branch: a kernel argument)
+                const u32x4 d = __builtin_nontemporal_load(&in.xdp[i]);
+                const uint64_t a = (uint64_t)d[1] << 32 | d[0];
+                const uint64_t off = (a & ((1ull << 48) - 1)) + (a >> 48);
+                meta = d[2];
+                plen = d[2];
+                ifx = in.xdp_ifindex;
+                sa.x = (uint32_t)off;
+                sa.y = (uint32_t)(off >> 32);
+            } else if (i < n) {
                 meta = __builtin_nontemporal_load(&in.linear_len[i]);
                 ifx = __builtin_nontemporal_load(&in.ifindex[i]);
                 plen = in.pkt_len ? __builtin_nontemporal_load(&in.pkt_len[i]) : meta;
@@ -1110,6 +1123,10 @@ BatchIn batch_of(const infw_launch_args &a) {
         const infw_batch_soa_c *c = a.compact;
         bi.saddr4 = c->saddr4, bi.v6tail = c->v6tail, bi.ifindex = c->ifindex, bi.pkt_len = c->pkt_len;
         bi.meta = c->meta, bi.l4word = c->l4word;
+    } else if (a.input == INFW_INPUT_FRAMES && a.xdp) {
+        bi.frames = a.umem;
+        bi.xdp = reinterpret_cast<const u32x4 *>(a.xdp);
+        bi.xdp_ifindex = a.xdp_ifindex;
     } else if (a.input == INFW_INPUT_FRAMES) {
         const infw_frame_batch *f = a.frames;
         bi.ifindex = f->ifindex, bi.pkt_len = f->pkt_len, bi.frames = f->frames, bi.offsets = f->offsets;

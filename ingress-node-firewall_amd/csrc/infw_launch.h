@@ -19,6 +19,9 @@ struct infw_launch_args {
     const infw_batch_soa *soa;
     const infw_batch_soa_c *compact;
     const infw_frame_batch *frames;
+    const uint8_t *umem;             // INFW_INPUT_FRAMES from AF_XDP descriptors (infw_classify_xdp) ...
+    const infw_xdp_desc *xdp;        // ... when non-null: frames at umem + addr, one ifindex for the ring
+    uint32_t xdp_ifindex;
     uint64_t n;
     uint32_t *results;
     uint8_t *verdicts;

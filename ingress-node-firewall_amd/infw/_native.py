@@ -90,6 +90,11 @@ class FrameBatch(C.Structure):
                 ("pkt_len", C.c_void_p), ("ifindex", C.c_void_p)]
 
 
+class XdpDesc(C.Structure):
+    """struct infw_xdp_desc (include/infw.h) = linux/if_xdp.h struct xdp_desc, 16 B."""
+    _fields_ = [("addr", C.c_uint64), ("len", C.c_uint32), ("options", C.c_uint32)]
+
+
 class EventHdrSt(C.Structure):
     """struct event_hdr_st (ingress_node_firewall.h:58-64), 8 B packed."""
     _pack_ = 1
@@ -143,7 +148,7 @@ ABI_SYMBOLS = [
     "infw_classify_frames_ex",
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
     "infw_table_delete_batch", "infw_set_option", "infw_get_option", "infw_option_name", "infw_classify_variant",
-    "infw_kernel_variant_name",
+    "infw_kernel_variant_name", "infw_classify_xdp",
 ]
 ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
 INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES = 0, 1, 2  # INFW_INPUT_*
@@ -226,6 +231,8 @@ _sig = {
     "infw_option_name": (C.c_char_p, [C.c_int]),
     "infw_classify_variant": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]),
     "infw_kernel_variant_name": (C.c_char_p, [C.c_int]),
+    "infw_classify_xdp": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)

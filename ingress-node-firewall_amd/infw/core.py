@@ -327,6 +327,18 @@ class Classifier:
                                             verdicts.data_ptr() if verdicts is not None else None,
                                             C.byref(ex) if ex is not None else None, sp), "classify_frames")
 
+    def classify_xdp(self, umem, descs, n: int, ifindex: int, results=None, verdicts=None, dev: int = 0,
+                     stream=None) -> None:
+        """infw_classify_xdp: an AF_XDP RX ring's descriptors (`descs`: n x 16 B, struct xdp_desc) over the frames of
+        `umem` — torch tensors in HBM or pinned host memory (read in place over PCIe); one ifindex for the ring."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(results.device if results is not None else torch.device("cuda", dev))
+        sp = stream if isinstance(stream, int) else stream.cuda_stream
+        check(N.lib.infw_classify_xdp(self._ctx, dev, umem.data_ptr(), descs.data_ptr(), n, ifindex,
+                                      results.data_ptr() if results is not None else None,
+                                      verdicts.data_ptr() if verdicts is not None else None, sp), "classify_xdp")
+
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
         """The perf samples of the deny events classify_events wrote (kernel.c:392-399) from the frames the batch was
