@@ -20,7 +20,12 @@ run cfg2_distinct --templates 1000000 --no-cpu-baseline --steps 20
 run cfg2_distinct_popularity_order --templates 1000000 --key-order workload --no-cpu-baseline --steps 20
 run cfg2_frames --from-frames 128 --no-cpu-baseline --steps 20
 run cfg2_frames_fused --from-frames 128 --fused --no-cpu-baseline --steps 20
+run cfg2_xdp_hbm --xdp-ring hbm --no-cpu-baseline --steps 20
+run cfg2_xdp_host --xdp-ring host --no-cpu-baseline --steps 10 --warmup 2
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
+# the library's one-process shape: one context over N device slots (all on this GPU), a thread + stream per slot
+run inproc_n1 --in-process --gpus 1 --slots-on-gpu0 --global-packets 1073741824 --steps 5 --warmup 1 --no-line-rates
+run inproc_n8 --in-process --gpus 8 --slots-on-gpu0 --global-packets 1073741824 --steps 5 --warmup 1 --no-line-rates
 for f in $OUT/*.log; do
-  python3 -c "import json; l=[x for x in open('$f') if x.startswith('{')]; d=json.loads(l[-1]); r=d['roofline']; print('$(basename $f .log)', d['value'], r['kernel_ms_avg'], r['frac'], r.get('from_frames', {}).get('pack_kernel_ms_avg', ''))"
+  python3 -c "import json; l=[x for x in open('$f') if x.startswith('{')]; d=json.loads(l[-1]); r=d.get('roofline', {}); print('$(basename $f .log)', d['value'], r.get('kernel_ms_avg', [s['kernel_ms_avg'] for s in d.get('per_slot', [])]), r.get('frac', ''), r.get('from_frames', {}).get('pack_kernel_ms_avg', ''), d['config'].get('stats_digest', '')[:12])"
 done
