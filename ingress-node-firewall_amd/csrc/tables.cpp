@@ -899,7 +899,7 @@ int compile_tables(const PendingMap &m, HostTables &out, const Options &opt, Inc
     // reference loader's Go map order) the hot lists' lines spread over all of it and every dependent
     // decision-line read pays for the span: 4 parts (1.8 GB, a leaf line for busy parts) 3.75 ms against
     // 5.03 at 16 (profiles/r03r; round 2's 16-part choice, profiles/r02b, was measured with the keys in
-    // popularity order, where the hot lists sit together); INFW_DT_PARTS=1|2|4|8|16 forces one form
+    // popularity order, where the hot lists sit together); the option dt_parts = 1|2|4|8|16 forces one form
     {
         std::vector<const uint8_t *> vals;
         vals.reserve(list_of_vid.size());

@@ -8,7 +8,7 @@
 #   lines        every bench.py workload line (tools/bench_all.sh)
 #   line:<key>   one workload line: key as in prof:<key>
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
-#                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512
+#                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512 xdphbm frames
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
 #   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: keyorder split fstride)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
@@ -28,6 +28,7 @@ args_of() {  # bench.py arguments of a workload key
     cfg2d)  echo "--templates 1000000" ;;
     cfg2dw) echo "--templates 1000000 --key-order workload" ;;
     cfg2w)  echo "--key-order workload" ;;
+    xdphbm) echo "--xdp-ring hbm" ;;
     fused80)  echo "--from-frames 80 --fused" ;;
     fused256) echo "--from-frames 256 --fused" ;;
     fused512) echo "--from-frames 512 --fused" ;;
