@@ -668,8 +668,9 @@ def run_rank(args):
             # are taken out of the L2 misses, not priced as random misses.  frac = that bound / the kernel time.
             if rates and "l2_hits_per_packet" in tj:
                 h, m = tj["l2_hits_per_packet"], tj["l2_misses_per_packet"]
-                stream_in = {"standard": 32.0, "compact": algo_bytes - 4, "frames": 12.0 + 128.0}[args.layout]
-                s_lines = (12.0 / 128 + 1.0) if args.layout == "frames" else stream_in / 128
+                side = 16.0 if args.xdp_ring else 12.0  # per frame: the descriptor, or lengths + ifindex
+                stream_in = {"standard": 32.0, "compact": algo_bytes - 4, "frames": side + 128.0}[args.layout]
+                s_lines = (side / 128 + 1.0) if args.layout == "frames" else stream_in / 128
                 tm = max(0.0, m - s_lines)
                 per_pkt_s = (h / (rates["l2_hit_G_per_s"] * 1e9) + tm / (rates["l2_miss_G_per_s"] * 1e9) +
                              (stream_in + 4) / (rates["stream_GB_per_s"] * 1e9))

@@ -41,6 +41,11 @@ def main():
         key += "_compact"
     if line:
         n = line["config"]["packets_per_gpu_per_step"]
+        # an AF_XDP line launches once per interface ring: a launch classifies 1 / rings of the step's frames on
+        # average, which is what the per-launch PMC averages below are divided by
+        rings = line.get("roofline", {}).get("xdp_ring", {}).get("rings")
+        if rings:
+            n = n / rings
     stream_b = 32.0  # tuple bytes read per packet
     if layout == "compact":
         stream_b = line["roofline"]["algorithmic_bytes_per_packet"] - 4
