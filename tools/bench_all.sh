@@ -1,10 +1,13 @@
 #!/bin/bash
-# Every bench.py workload line on the current build (on the GPU box).  Usage: tools/bench_all.sh <out_dir>
+# Every bench.py workload line on the current build (on the GPU box).  Usage: tools/bench_all.sh <out_dir> [names]
 set -u
 OUT=${1:-gpurun_out/bench_all}
+shift || true
+ONLY=" $* "  # optional: the line names to run (default: all)
 mkdir -p $OUT
 run() {  # name, args...
   local name=$1; shift
+  if [ "$ONLY" != "  " ] && [[ "$ONLY" != *" $name "* ]]; then return 0; fi
   timeout -k 10 300 python bench.py "$@" > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"

@@ -5,7 +5,7 @@
 #   suite        pytest -m gpu (as the driver runs it, with per-test timeouts) and __graft_entry__.smoke()
 #   test:<expr>  pytest -m gpu -k <expr> (one test group)
 #   bench        the default bench line (what the driver's BENCH record runs)
-#   lines        every bench.py workload line (tools/bench_all.sh)
+#   lines        every bench.py workload line (tools/bench_all.sh); lines:<a,b,..> a subset
 #   line:<key>   one workload line: key as in prof:<key>
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512 xdphbm frames
@@ -58,6 +58,8 @@ step() {
       tail -1 $O/bench_default.log | cut -c1-400 ;;
     lines)
       bash tools/bench_all.sh $O/lines || rc=$? ;;
+    lines:*)  # a comma-separated subset of tools/bench_all.sh's lines
+      bash tools/bench_all.sh $O/lines $(echo ${s#lines:} | tr , ' ') || rc=$? ;;
     line:*)
       local a; a=$(args_of ${s#line:}) || return 2
       timeout -k 10 300 python -u bench.py $a --no-cpu-baseline > $O/line_${s#line:}.log 2>&1 || rc=$?
