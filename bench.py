@@ -612,8 +612,8 @@ def run_rank(args):
         assert torch.equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
     digest = stats_digest(digest_block.cpu().numpy())
     # the registry name of the instantiation(s) this line ran (infw_classify_variant: the library's own selector)
-    kernel = clf.variant({"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
-                          "frames": infw.INPUT_FRAMES}[args.layout])
+    kernel = clf.variant(infw.INPUT_XDP if args.xdp_ring else {"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
+                                                               "frames": infw.INPUT_FRAMES}[args.layout])
     if args.xdp_ring:
         extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "chunk": stride, "rings": len(rings),
                                    "frames_per_ring": [r[1] for r in rings],

@@ -309,13 +309,15 @@ const char *infw_option_name(int i);
 
 /* Which kernel instantiation(s) a launch would run (introspection; nothing is */
 /* launched, no device needed — host-only contexts answer from their image).  */
-/* input: INFW_INPUT_*; flags: INFW_VARIANT_EVENTS for an infw_classify_ex     */
-/* event stream (the debug sideband follows infw_debug_lookup_set).  name is a */
-/* registry name (infw_kernel_variant_name); two-phase launches name both      */
-/* kernels joined by '+'.  -ERANGE when cap is too small.                      */
+/* input: INFW_INPUT_* (XDP: infw_classify_xdp); flags: INFW_VARIANT_EVENTS   */
+/* for an infw_classify_ex event stream (not with COMPACT or XDP); the debug   */
+/* sideband follows infw_debug_lookup_set.  name is a registry name           */
+/* (infw_kernel_variant_name); two-phase launches name both kernels joined by */
+/* '+'.  -ERANGE when cap is too small.                                        */
 #define INFW_INPUT_SOA 0
 #define INFW_INPUT_COMPACT 1
 #define INFW_INPUT_FRAMES 2
+#define INFW_INPUT_XDP 3
 #define INFW_VARIANT_EVENTS 0x1u
 int infw_classify_variant(infw_ctx *ctx, int dev, int input, uint32_t flags, char *name, size_t cap);
 /* Registry of every kernel instantiation the library launches: name of entry */

@@ -476,7 +476,8 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(const infw_dev_tables T,
 // One instantiation per selectable variant (the registry below):
 //   kWaves   minimum waves per SIMD the register allocation must allow (8 = four 512-thread workgroups per CU;
 //            6 leaves room for 104 SGPRs, no spills);
-//   kIn      batch form: 0 SoA tuples (infw_batch_soa), 1 family-compact (infw_batch_soa_c), 2 raw frames;
+//   kIn      batch form: 0 SoA tuples (infw_batch_soa), 1 family-compact (infw_batch_soa_c), 2 raw frames,
+//            3 raw frames named by AF_XDP descriptors (its own instantiation: the frames kernel keeps no branch);
 //   kC24Log  LDS word cache of 1 << kC24Log entries (workgroups of >= 384 threads), kB6Log the IPv6 group cache
 //            (0: none);
 //   kEvents / kDebug  the deny-event and debug-lookup sidebands;
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                                                           uint8_t *__restrict__ verdicts,
                                                           unsigned long long *__restrict__ stats,
                                                           const Sideband sb) {
-    constexpr bool kC = kIn == 1, kF = kIn == 2;
+    constexpr bool kC = kIn == 1, kF = kIn == 2 || kIn == 3, kX = kIn == 3;
     const EventSink &ev = sb.ev;
     // per-workgroup counters [rule][allow=0, deny=1], packets << 40 | bytes in one u64 (one LDS atomic per update):
     // only frames shorter than kBigLen take this path and the workgroup flushes every kFlushTiles tiles, so
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
     auto load_tuple = [&](uint64_t i, uint32_t &meta, uint32_t &l4w, uint32_t &ifx, uint32_t &plen, uint4 &sa,
                           bool with_meta = true) {
         if (kF) {  // frames: linear length (meta), frame byte offset (sa.x/sa.y), ifindex, frame length
-            if (i < n && in.xdp) {  // one 16-B descriptor per frame (a uniform branch: a kernel argument)
+            if (kX && i < n) {  // one 16-B descriptor per frame
                 const u32x4 d = __builtin_nontemporal_load(&in.xdp[i]);
                 const uint64_t a = (uint64_t)d[1] << 32 | d[0];
                 const uint64_t off = (a & ((1ull << 48) - 1)) + (a >> 48);
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void classify_kernel(const infw_dev
                 ifx = in.xdp_ifindex;
                 sa.x = (uint32_t)off;
                 sa.y = (uint32_t)(off >> 32);
-            } else if (i < n) {
+            } else if (!kX && i < n) {
                 meta = __builtin_nontemporal_load(&in.linear_len[i]);
                 ifx = __builtin_nontemporal_load(&in.ifindex[i]);
                 plen = in.pkt_len ? __builtin_nontemporal_load(&in.pkt_len[i]) : meta;
@@ -989,7 +990,7 @@ constexpr Variant V() {
                    &run<kBlock, G, kWaves, kIn, kLog, kB6, kEv, kDbg, kLean, kPl, kD16, kSplit, kHalf>};
 }
 constexpr bool F = false, T_ = true;
-constexpr int S = INFW_INPUT_SOA, C = INFW_INPUT_COMPACT, R = INFW_INPUT_FRAMES;
+constexpr int S = INFW_INPUT_SOA, C = INFW_INPUT_COMPACT, R = INFW_INPUT_FRAMES, X = INFW_INPUT_XDP;
 
 // LDS per workgroup of the 768-thread shapes: the word cache (8 B x 2^log) and the IPv6 group cache (32 B x 2^b6)
 // take what the counters (2 KiB), the ifindex map (2 KiB), the per-list part counts (16 KiB, pl) and the frame
@@ -1044,12 +1045,20 @@ static const Variant kVariants[] = {
     V<512, 0, 6, R, 10, 0, T_, F, F, F, F, F, F>(),
     V<512, 0, 6, R, 10, 0, F, T_, F, F, F, F, F>(),
     V<512, 0, 6, R, 10, 0, T_, T_, F, F, F, F, F>(),
+    // AF_XDP descriptors over a umem: as raw frames (no event stream: infw_classify_xdp has none)
+    V<768, 0, 6, X, 11, 9, F, F, F, F, F, F, F>(),
+    V<768, 0, 6, X, 10, 9, F, F, F, T_, F, F, F>(),
+    V<768, 0, 6, X, 11, 9, F, F, T_, F, F, F, F>(),
+    V<768, 0, 6, X, 10, 9, F, F, T_, T_, F, F, F>(),
+    V<768, 0, 6, X, 11, 9, F, F, T_, F, T_, F, F>(),
+    V<768, 0, 6, X, 10, 9, F, F, T_, T_, T_, F, F>(),
+    V<512, 0, 6, X, 10, 0, F, T_, F, F, F, F, F>(),
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kDecideBlock = 512, kDecideBpc = 2;  // decide_kernel: 2 x 512 per CU (profiles/r04e: 40.3 vs 39.1 Gpps at 4)
 
 void variant_name(const VKey &k, char *buf, size_t cap) {
-    static const char *const in[] = {"soa", "compact", "frames"};
+    static const char *const in[] = {"soa", "compact", "frames", "xdp"};
     snprintf(buf, cap, "%s.%u.w%u.g%u.c%u.b%u%s%s%s%s%s%s%s", in[k.in], k.block, k.waves, k.group, k.log, k.b6log,
              k.lean ? ".lean" : "", k.pl ? ".pl" : "", k.d16 ? ".d16" : "", k.half ? ".half" : "",
              k.split ? ".split" : "", k.ev ? ".ev" : "", k.dbg ? ".dbg" : "");
@@ -1076,7 +1085,7 @@ VKey select_variant(const infw_launch_args &a, bool allow_split, uint32_t *bpc) 
         *bpc = 3;
         return k;
     }
-    if (a.input == INFW_INPUT_FRAMES) {  // any shape: 768 x 2
+    if (a.input == INFW_INPUT_FRAMES || a.input == INFW_INPUT_XDP) {  // any shape: 768 x 2
         k.block = 768, k.waves = 6, k.b6log = 9, k.log = pl ? 10 : 11;
         k.lean = lean, k.pl = pl, k.d16 = lean && d16;
         *bpc = 2;
@@ -1123,7 +1132,7 @@ BatchIn batch_of(const infw_launch_args &a) {
         const infw_batch_soa_c *c = a.compact;
         bi.saddr4 = c->saddr4, bi.v6tail = c->v6tail, bi.ifindex = c->ifindex, bi.pkt_len = c->pkt_len;
         bi.meta = c->meta, bi.l4word = c->l4word;
-    } else if (a.input == INFW_INPUT_FRAMES && a.xdp) {
+    } else if (a.input == INFW_INPUT_XDP) {
         bi.frames = a.umem;
         bi.xdp = reinterpret_cast<const u32x4 *>(a.xdp);
         bi.xdp_ifindex = a.xdp_ifindex;

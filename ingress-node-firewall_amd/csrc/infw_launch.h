@@ -15,12 +15,12 @@
 
 struct infw_launch_args {
     const infw_dev_tables *T;      // the epoch's view, split / stat_flush_tiles already decided by the caller
-    int input;                     // INFW_INPUT_SOA / _COMPACT / _FRAMES (include/infw.h)
+    int input;                     // INFW_INPUT_SOA / _COMPACT / _FRAMES / _XDP (include/infw.h)
     const infw_batch_soa *soa;
     const infw_batch_soa_c *compact;
     const infw_frame_batch *frames;
-    const uint8_t *umem;             // INFW_INPUT_FRAMES from AF_XDP descriptors (infw_classify_xdp) ...
-    const infw_xdp_desc *xdp;        // ... when non-null: frames at umem + addr, one ifindex for the ring
+    const uint8_t *umem;             // INFW_INPUT_XDP (infw_classify_xdp): AF_XDP descriptors, frames at
+    const infw_xdp_desc *xdp;        // umem + addr, one ifindex for the ring
     uint32_t xdp_ifindex;
     uint64_t n;
     uint32_t *results;

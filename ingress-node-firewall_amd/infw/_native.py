@@ -151,7 +151,7 @@ ABI_SYMBOLS = [
     "infw_kernel_variant_name", "infw_classify_xdp",
 ]
 ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
-INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES = 0, 1, 2  # INFW_INPUT_*
+INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES, INPUT_XDP = 0, 1, 2, 3  # INFW_INPUT_*
 VARIANT_EVENTS = 0x1  # INFW_VARIANT_EVENTS
 
 

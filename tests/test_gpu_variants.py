@@ -33,6 +33,15 @@ def test_every_registered_variant_matches_the_oracle():
     n, start, stride = (1 << 18) + 37, 4242, 128
     hdr, cap, pl, ifx = wl.frames(start, n)
     ores, over, ostats, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    # the same frames as an AF_XDP ring (infw_classify_xdp): one ifindex for the ring, the descriptor's length as
+    # both the linear and the frame length, the 80-B snapshots back to back in a umem in HBM
+    ring_if = int(np.bincount(ifx).argmax())
+    xres, xver, xstats, _ = m.classify_frames(hdr, pl.astype(cap.dtype), pl, np.full(n, ring_if, np.uint32), nthreads=8)
+    addr = np.arange(n, dtype=np.uint64) * np.uint64(hdr.shape[1])
+    desc = np.zeros((n, 4), np.uint32)
+    desc[:, 0], desc[:, 1], desc[:, 2] = addr & np.uint64(0xFFFFFFFF), addr >> np.uint64(32), pl
+    umem = torch.from_numpy(np.concatenate([hdr.reshape(-1), np.zeros(64, np.uint8)])).to(dev)
+    xdesc = torch.from_numpy(desc.view(np.int32)).to(dev)
     deny = int(((ores & 0xFF) == infw.XDP_DROP).sum())
     batch = SoaBatch.empty(n, dev)
     wl.gen_device(batch, start, 0)
@@ -73,16 +82,19 @@ def test_every_registered_variant_matches_the_oracle():
                     clf.classify(batch, results=res, verdicts=ver)
             elif inp == "compact":
                 clf.classify_c(bc, results=res, verdicts=ver)
+            elif inp == "xdp":
+                clf.classify_xdp(umem, xdesc, n, ring_if, results=res, verdicts=ver)
             else:
                 clf.classify_frames(frames, lin, fifx, n, results=res, verdicts=ver, pkt_len=plen, stride=stride,
                                     **evs)
             torch.cuda.synchronize()
             label = f"{name} ({kind}, split={split}, shape={shape}, {inp}, ev={ev}, dbg={dbg})"
+            wres, wver, wstats = (xres, xver, xstats) if inp == "xdp" else (ores, over, ostats)
             gres = res.cpu().numpy().view(np.uint32)
-            bad = np.nonzero(gres != ores)[0]
+            bad = np.nonzero(gres != wres)[0]
             assert bad.size == 0, f"{label}: {bad.size} result words differ, first {bad[:4]}"
-            assert np.array_equal(ver.cpu().numpy(), over), f"{label}: verdicts"
-            assert np.array_equal(clf.stats_read_all(), ostats), f"{label}: counters"
+            assert np.array_equal(ver.cpu().numpy(), wver), f"{label}: verdicts"
+            assert np.array_equal(clf.stats_read_all(), wstats), f"{label}: counters"
             if ev:
                 assert int(events_count.item()) == deny, label
             if dbg:

@@ -27,7 +27,7 @@ KINDS = {
 # every launch shape infw_set_launch accepts: (block, scan_group, blocks_per_cu)
 SHAPES = [(768, 0, 2), (512, 0, 2), (512, 0, 3), (512, 0, 4), (256, 0, 6),
           (512, 1, 3), (512, 4, 3), (512, 8, 3), (256, 1, 6), (256, 4, 6), (256, 8, 6)]
-INPUTS = {"soa": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT, "frames": infw.INPUT_FRAMES}
+INPUTS = {"soa": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT, "frames": infw.INPUT_FRAMES, "xdp": infw.INPUT_XDP}
 # a small configs[2]-shaped table: 16 value parts (so per-list part counts exist), IPv4 and IPv6 entries
 TABLE = dict(n_prefixes=20000, n_templates=64)
 
@@ -36,8 +36,8 @@ def scenarios():
     """(kind, split, shape, input name, events, debug) of every launch worth asking about."""
     for kind, split, shape, inp, ev, dbg in itertools.product(KINDS, (0, 1), SHAPES, INPUTS, (False, True),
                                                               (False, True)):
-        if inp == "compact" and ev:
-            continue  # infw_classify_c has no event stream
+        if inp in ("compact", "xdp") and ev:
+            continue  # infw_classify_c and infw_classify_xdp have no event stream
         yield kind, split, shape, inp, ev, dbg
 
 
