@@ -114,3 +114,17 @@ def test_library_reads_no_environment():
     import subprocess
     out = subprocess.run(["nm", "-D", "--undefined-only", infw.LIB_PATH], capture_output=True, text=True).stdout
     assert "getenv" not in out and "secure_getenv" not in out
+
+
+def test_variant_arguments_validated():
+    """infw_classify_variant: inputs past INFW_INPUT_XDP, unknown flags and an event stream on the family-compact
+    or AF_XDP forms (infw_classify_c / infw_classify_xdp have none) are -EINVAL; the AF_XDP form names its own
+    instantiations (xdp.*), the frames form its own (frames.*)."""
+    c = _ctx("lean.pl")
+    assert c.variant(infw.INPUT_XDP).startswith("xdp.768.")
+    assert c.variant(infw.INPUT_FRAMES).startswith("frames.768.")
+    for inp, ev in [(infw.INPUT_XDP, True), (infw.INPUT_COMPACT, True), (4, False), (-1, False)]:
+        with pytest.raises(infw.InfwError) as e:
+            c.variant(inp, events=ev)
+        assert e.value.errno == 22, (inp, ev)
+    c.close()
