@@ -330,10 +330,12 @@ class Classifier:
     def classify_xdp(self, umem, descs, n: int, ifindex: int, results=None, verdicts=None, dev: int = 0,
                      stream=None) -> None:
         """infw_classify_xdp: an AF_XDP RX ring's descriptors (`descs`: n x 16 B, struct xdp_desc) over the frames of
-        `umem` — torch tensors in HBM or pinned host memory (read in place over PCIe); one ifindex for the ring."""
+        `umem` — torch tensors in HBM or pinned host memory (read in place over PCIe); one ifindex for the ring.
+        `results` / `verdicts` may be device or pinned host tensors."""
         if stream is None:
             import torch
-            stream = torch.cuda.current_stream(results.device if results is not None else torch.device("cuda", dev))
+            on = results.device if results is not None and results.is_cuda else torch.device("cuda", dev)
+            stream = torch.cuda.current_stream(on)  # results / verdicts may be pinned host memory
         sp = stream if isinstance(stream, int) else stream.cuda_stream
         check(N.lib.infw_classify_xdp(self._ctx, dev, umem.data_ptr(), descs.data_ptr(), n, ifindex,
                                       results.data_ptr() if results is not None else None,

@@ -75,6 +75,32 @@ def test_xdp_ring_matches_oracle(where, mode):
     assert (want & 0xFF).astype(bool).mean() > 0.3  # the frames exercise the rules
 
 
+def test_xdp_results_in_host_memory():
+    """A daemon may take the verdicts straight into pinned host memory: umem, ring, result
+    words and verdicts all in pinned host memory, the kernel reading and writing over PCIe."""
+    rng = np.random.default_rng(11)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    n = (1 << 13) + 5
+    hdr, cap, pl, ifx = wl.frames(777, n)
+    ring_if = int(np.bincount(ifx).argmax())
+    want, wver, wst, _ = oracle_for(wl).classify_frames(hdr, pl.astype(cap.dtype), pl, np.full(n, ring_if, np.uint32),
+                                                        nthreads=8)
+    umem, desc = _ring(hdr, pl, "aligned", rng)
+    tu = torch.from_numpy(umem).pin_memory()
+    td = torch.from_numpy(desc.view(np.int32)).pin_memory()
+    res = torch.full((n,), -1, dtype=torch.int32).pin_memory()
+    ver = torch.full((n,), 7, dtype=torch.uint8).pin_memory()
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    clf.stats_reset()
+    clf.classify_xdp(tu, td, n, ring_if, results=res, verdicts=ver)
+    torch.cuda.synchronize()
+    assert np.array_equal(res.numpy().view(np.uint32), want)
+    assert np.array_equal(ver.numpy(), wver)
+    assert np.array_equal(clf.stats_read_all(), wst)
+
+
 def test_xdp_rejects_bad_arguments():
     clf = infw.Classifier(devices=[0])
     dev = torch.device("cuda", 0)
