@@ -1,0 +1,159 @@
+/*
+ * xdp_demo.c — the AF_XDP side of the boundary driven from plain C, the way a node daemon would
+ * (INTEGRATION.md §1.1.2): the umem is the daemon's own memory (posix_memalign, as it would hand it to
+ * XDP_UMEM_REG), page-locked for the GPU with infw_host_register; the RX ring's descriptors name frames in it;
+ * infw_classify_xdp reads the frames and the descriptors in place over PCIe and writes the result words and verdicts
+ * into the daemon's (registered) host arrays.  One ring per interface queue: the frames of ifindex 7 and of ifindex
+ * 8 are two calls.
+ *
+ *   the XDP entry per frame (kernel.c:459-462, ethertype / L4 extraction :95-174, :412-440)
+ *   statsMap.Lookup (statistics.go:127):  infw_stats_read
+ *
+ * Built by tests/test_c_abi.py (gcc against include/infw.h and the HIP runtime's header for the stream sync).
+ * `xdp_demo host` runs without a GPU: an INFW_F_HOST_ONLY context, whose infw_classify_xdp must refuse (-ENODEV).
+ * Prints "xdp_demo OK ..." and exits 0 when every verdict and counter is the expected one.
+ */
+#define _POSIX_C_SOURCE 200112L /* posix_memalign */
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "infw.h"
+
+#define CHECK(call)                                                                                 \
+    do {                                                                                            \
+        int rc_ = (call);                                                                           \
+        if (rc_ < 0) {                                                                              \
+            fprintf(stderr, "%s failed: %d (%s)\n", #call, rc_, infw_last_error());                 \
+            return 1;                                                                               \
+        }                                                                                           \
+    } while (0)
+
+enum { CHUNK = 2048, HEADROOM = 256, N = 6, CHUNKS = 16 };
+
+/* An Ethernet + IPv4 + TCP/UDP frame of `len` bytes at f: the bytes kernel.c reads (ethertype, protocol, saddr,
+ * destination port at L4 offset 34). */
+static void put_frame(uint8_t *f, const uint8_t ip[4], uint8_t proto, uint16_t dport, uint32_t len) {
+    memset(f, 0, len);
+    f[12] = 0x08, f[13] = 0x00;     /* ETH_P_IP */
+    f[14] = 0x45;                   /* version 4, IHL 5 */
+    f[16] = (uint8_t)((len - 14) >> 8), f[17] = (uint8_t)(len - 14);
+    f[22] = 64, f[23] = proto;      /* ttl, protocol */
+    memcpy(f + 26, ip, 4);          /* saddr */
+    f[30] = 198, f[31] = 51, f[32] = 100, f[33] = 1;
+    f[34] = 40000 >> 8, f[35] = 40000 & 0xFF;  /* source port */
+    f[36] = dport >> 8, f[37] = dport & 0xFF;  /* destination port */
+}
+
+int main(int argc, char **argv) {
+    const int host_only = argc > 1 && strcmp(argv[1], "host") == 0;
+    infw_ctx *ctx = NULL;
+    CHECK(infw_create(&ctx, NULL, 0, 1024, host_only ? INFW_F_HOST_ONLY : 0));
+
+    /* eth0 (ifindex 7): 10.0.0.0/8 -> [order 1: TCP 80 Deny, order 2: TCP 1-1024 Allow]; 192.0.2.0/24 -> UDP 53 Allow */
+    struct lpm_ip_key_st key;
+    struct rulesVal_st val;
+    memset(&val, 0, sizeof(val));
+    CHECK(infw_build_ebpf_key(7, "10.0.0.0/8", &key));
+    CHECK(infw_make_rule(&val, 1, "TCP", "80", 0, 0, "Deny"));
+    CHECK(infw_make_rule(&val, 2, "TCP", "1-1024", 0, 0, "Allow"));
+    CHECK(infw_table_update(ctx, &key, &val, INFW_BPF_ANY));
+    memset(&val, 0, sizeof(val));
+    CHECK(infw_build_ebpf_key(7, "192.0.2.0/24", &key));
+    CHECK(infw_make_rule(&val, 3, "UDP", "53", 0, 0, "Allow"));
+    CHECK(infw_table_update(ctx, &key, &val, INFW_BPF_ANY));
+    CHECK(infw_table_commit(ctx));
+
+    /* the daemon's umem and ring memory, page-aligned as XDP_UMEM_REG wants it */
+    uint8_t *umem = NULL;
+    struct infw_xdp_desc *rx = NULL;
+    uint32_t *results = NULL;
+    uint8_t *verdicts = NULL;
+    if (posix_memalign((void **)&umem, 4096, CHUNKS * CHUNK) || posix_memalign((void **)&rx, 4096, 4096) ||
+        posix_memalign((void **)&results, 4096, 4096) || posix_memalign((void **)&verdicts, 4096, 4096)) {
+        fprintf(stderr, "posix_memalign failed\n");
+        return 1;
+    }
+    memset(umem, 0, CHUNKS * CHUNK);
+    const uint8_t a[4] = {10, 1, 2, 3}, b[4] = {192, 0, 2, 9}, c[4] = {11, 0, 0, 1};
+    /* packet i in chunk 2i+1 (a fill ring hands chunks out in any order), frame at chunk + headroom;
+     * the last one arrives on the other interface's queue */
+    const struct { const uint8_t *ip; uint8_t proto; uint16_t dport; uint32_t len; } pk[N] = {
+        {a, 6, 80, 100},   /* rule 1: DROP  */
+        {a, 6, 443, 200},  /* rule 2: PASS  */
+        {a, 6, 2000, 300}, /* no rule: PASS */
+        {b, 17, 53, 400},  /* rule 3: PASS  */
+        {c, 6, 80, 500},   /* no prefix     */
+        {a, 6, 80, 600},   /* ifindex 8: no entry */
+    };
+    for (int i = 0; i < N; i++) {
+        const uint64_t at = (uint64_t)(2 * i + 1) * CHUNK + HEADROOM;
+        put_frame(umem + at, pk[i].ip, pk[i].proto, pk[i].dport, pk[i].len);
+        rx[i].addr = at;
+        rx[i].len = pk[i].len;
+        rx[i].options = 0;
+    }
+    if (host_only) {
+        const int rc = infw_classify_xdp(ctx, 0, umem, rx, N - 1, 7, results, verdicts, NULL);
+        if (rc != -ENODEV) {
+            fprintf(stderr, "host-only classify_xdp returned %d, want -ENODEV\n", rc);
+            return 1;
+        }
+        infw_destroy(ctx);
+        printf("xdp_demo OK (host): classify_xdp refused without a device, ABI %d\n", infw_abi_version());
+        return 0;
+    }
+    CHECK(infw_host_register(ctx, umem, CHUNKS * CHUNK));
+    CHECK(infw_host_register(ctx, rx, 4096));
+    CHECK(infw_host_register(ctx, results, 4096));
+    CHECK(infw_host_register(ctx, verdicts, 4096));
+    memset(results, 0xFF, 4 * N);
+    memset(verdicts, 7, N);
+    /* ring of ifindex 7: descriptors 0..4; ring of ifindex 8: descriptor 5 (NULL stream: the default one) */
+    CHECK(infw_classify_xdp(ctx, 0, umem, rx, N - 1, 7, results, verdicts, NULL));
+    CHECK(infw_classify_xdp(ctx, 0, umem, rx + N - 1, 1, 8, results + N - 1, verdicts + N - 1, NULL));
+    if (hipDeviceSynchronize() != hipSuccess) {
+        fprintf(stderr, "hipDeviceSynchronize failed\n");
+        return 1;
+    }
+    const uint32_t want_r[N] = {INFW_RESULT(INFW_XDP_DROP, 1), INFW_RESULT(INFW_XDP_PASS, 2), 0,
+                                INFW_RESULT(INFW_XDP_PASS, 3), 0, 0};
+    const uint8_t want_v[N] = {INFW_XDP_DROP, INFW_XDP_PASS, INFW_XDP_PASS, INFW_XDP_PASS, INFW_XDP_PASS, INFW_XDP_PASS};
+    for (int i = 0; i < N; i++)
+        if (verdicts[i] != want_v[i] || results[i] != want_r[i]) {
+            fprintf(stderr, "frame %d: verdict %u result 0x%x, want %u 0x%x\n", i, verdicts[i], results[i],
+                    want_v[i], want_r[i]);
+            return 1;
+        }
+    /* per-rule counters (bytes = the descriptor's frame length, bpf_xdp_get_buff_len) */
+    struct ruleStatistics_st st[8];
+    int slots = 0;
+    uint64_t allow = 0, deny = 0, allow_b = 0, deny_b = 0;
+    for (uint32_t rule = 1; rule < 100; rule++) {
+        CHECK(infw_stats_read(ctx, rule, st, &slots));
+        for (int s = 0; s < slots; s++) {
+            allow += st[s].allow_stats.packets;
+            allow_b += st[s].allow_stats.bytes;
+            deny += st[s].deny_stats.packets;
+            deny_b += st[s].deny_stats.bytes;
+        }
+    }
+    if (allow != 2 || allow_b != 600 || deny != 1 || deny_b != 100) {
+        fprintf(stderr, "counters: allow %llu/%llu deny %llu/%llu\n", (unsigned long long)allow,
+                (unsigned long long)allow_b, (unsigned long long)deny, (unsigned long long)deny_b);
+        return 1;
+    }
+    CHECK(infw_host_unregister(ctx, umem));
+    CHECK(infw_host_unregister(ctx, rx));
+    CHECK(infw_host_unregister(ctx, results));
+    CHECK(infw_host_unregister(ctx, verdicts));
+    infw_destroy(ctx);
+    free(umem), free(rx), free(results), free(verdicts);
+    printf("xdp_demo OK: %d frames in 2 rings, allow %llu (%llu B), deny %llu (%llu B), ABI %d\n", N,
+           (unsigned long long)allow, (unsigned long long)allow_b, (unsigned long long)deny,
+           (unsigned long long)deny_b, infw_abi_version());
+    return 0;
+}

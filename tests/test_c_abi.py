@@ -27,6 +27,39 @@ def build_demo(tmp_path):
     return exe
 
 
+def build_xdp_demo(tmp_path):
+    """tests/c/xdp_demo.c: plain C against include/infw.h, plus the HIP runtime's C header for the stream sync a
+    daemon does after infw_classify_xdp."""
+    cc = shutil.which("gcc") or shutil.which("cc")
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    if cc is None or not os.path.exists(os.path.join(rocm, "include", "hip", "hip_runtime_api.h")):
+        pytest.skip("no C compiler or HIP headers")
+    exe = str(tmp_path / "xdp_demo")
+    cmd = [cc, "-std=c11", "-O1", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I",
+           os.path.join(ROOT, "include"), "-I", os.path.join(rocm, "include"),
+           os.path.join(ROOT, "tests", "c", "xdp_demo.c"), "-o", exe, "-L", LIB_DIR, "-linfw",
+           "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath," + LIB_DIR + ":" + os.path.join(rocm, "lib")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_c_xdp_caller_host_only(tmp_path):
+    exe = build_xdp_demo(tmp_path)
+    out = subprocess.run([exe, "host"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("xdp_demo OK (host)")
+
+
+@pytest.mark.gpu
+def test_c_xdp_caller_on_device(tmp_path):
+    """A daemon's own (registered) umem, ring and result arrays through infw_classify_xdp, two interface rings."""
+    exe = build_xdp_demo(tmp_path)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "allow 2 (600 B), deny 1 (100 B)" in out.stdout
+
+
 def test_c_caller_host_only(tmp_path):
     exe = build_demo(tmp_path)
     out = subprocess.run([exe, "host"], capture_output=True, text=True, timeout=60)
