@@ -179,10 +179,11 @@ def parse(argv=None):
                     help="with --in-process: every slot on device 0 (rehearsal of the N-slot shape on one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="per-context option (include/infw.h) for every context this bench creates")
-    ap.add_argument("--xdp-ring", choices=("hbm", "host"), default=None,
+    ap.add_argument("--xdp-ring", choices=("hbm", "host", "registered"), default=None,
                     help="AF_XDP feed: the frames in a umem of 2048-B chunks (--from-frames sets another chunk size) "
-                         "in HBM or pinned host memory (read over PCIe), one RX descriptor ring per interface, "
-                         "classified by infw_classify_xdp (implies --fused)")
+                         "in HBM, in pinned host memory (hipHostMalloc) or in the process's own anonymous mapping "
+                         "page-locked with infw_host_register (what a daemon's XDP_UMEM_REG memory is), read over "
+                         "PCIe; one RX descriptor ring per interface, classified by infw_classify_xdp (implies --fused)")
     ap.add_argument("--fused", action="store_true",
                     help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
                          "no SoA batch written or read; checked untimed against the packer path's results")
@@ -510,6 +511,24 @@ def run_rank(args):
             frames = umem
             for r in rings:
                 r[2] = r[2].pin_memory()
+        elif args.xdp_ring == "registered":  # the daemon's own memory (an anonymous mapping), page-locked for the GPU
+            import mmap
+            registered = []
+
+            def own(nbytes):
+                mm = mmap.mmap(-1, max(nbytes, 4096))
+                arr = np.frombuffer(mm, dtype=np.uint8, count=nbytes)
+                clf.host_register(arr)
+                registered.append((mm, arr))
+                return torch.from_numpy(arr)
+            umem = own(frames.numel())
+            umem.copy_(frames)
+            del frames
+            frames = umem
+            for r in rings:
+                t = own(r[2].numel() * 4).view(torch.int32)
+                t.copy_(r[2].view(-1))
+                r[2] = t
         else:
             for r in rings:
                 r[2] = r[2].to(dev)
@@ -618,9 +637,13 @@ def run_rank(args):
         extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "chunk": stride, "rings": len(rings),
                                    "frames_per_ring": [r[1] for r in rings],
                                    "results_equal_packer_path": fused_check,
-                                   "note": "umem and descriptor rings in " + (
-                                       "pinned host memory, read by the kernel over PCIe (PCIe-inclusive rate)"
-                                       if args.xdp_ring == "host" else "HBM")}}
+                                   "note": "umem and descriptor rings in " + {
+                                       "host": "pinned host memory (hipHostMalloc), read by the kernel over PCIe "
+                                               "(PCIe-inclusive rate)",
+                                       "registered": "the process's own anonymous mapping page-locked with "
+                                                     "infw_host_register, read by the kernel over PCIe "
+                                                     "(PCIe-inclusive rate)",
+                                       "hbm": "HBM"}[args.xdp_ring]}}
     elif args.fused:
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,
                                       "results_equal_packer_path": fused_check}}

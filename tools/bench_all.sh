@@ -25,6 +25,7 @@ run cfg2_frames --from-frames 128 --no-cpu-baseline --steps 20
 run cfg2_frames_fused --from-frames 128 --fused --no-cpu-baseline --steps 20
 run cfg2_xdp_hbm --xdp-ring hbm --no-cpu-baseline --steps 20
 run cfg2_xdp_host --xdp-ring host --no-cpu-baseline --steps 10 --warmup 2
+run cfg2_xdp_registered --xdp-ring registered --no-cpu-baseline --steps 10 --warmup 2
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
 # the library's one-process shape: one context over N device slots (all on this GPU), a thread + stream per slot
 run inproc_n1 --in-process --gpus 1 --slots-on-gpu0 --global-packets 1073741824 --steps 5 --warmup 1 --no-line-rates
