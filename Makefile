@@ -14,7 +14,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-functi
 EXTRA    ?=
 
 LIB_SRCS := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp \
-            $(SRC)/classify.hip $(SRC)/pack.hip $(SRC)/patch.hip
+            $(SRC)/hostfeed.cpp $(SRC)/classify.hip $(SRC)/pack.hip $(SRC)/patch.hip
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
 HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
 
@@ -28,7 +28,7 @@ $(OBJ)/classify.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 # bench.py only attaches a profile's PMC figures to a line when the profile was taken on the same build id
 # (and a table image is accepted only by a library of the same build id, so every source that defines the serialised
 # layout — image.cpp's field order, infw_internal.h's HostTables / IncState, incremental.cpp's state — is in it)
-BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_launch.h $(SRC)/infw_pack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
+BUILDID_SRCS := $(SRC)/classify.hip $(SRC)/infw_tables.h $(SRC)/infw_launch.h $(SRC)/infw_pack.h $(SRC)/infw_hostpack.h $(SRC)/tables.cpp $(SRC)/pack.hip include/infw.h \
                 $(SRC)/image.cpp $(SRC)/infw_internal.h $(SRC)/incremental.cpp
 # The flags part is fixed when the Makefile is read (abi.cpp's, which compiles the id in): a target-specific HIPFLAGS
 # of whichever target first needs the header (classify.hip.o's, abi.cpp.o's, the sanitizer objects') must not change it.
@@ -46,7 +46,7 @@ $(OBJ)/%.o: $(SRC)/% $(HDRS)
 
 $(OUT)/libinfw.so: $(LIB_OBJS)
 	@mkdir -p $(OUT)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(LIB_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(LIB_OBJS)
 
 $(OUT)/libinfw_workload.so: $(OBJ)/workload.hip.o
 	@mkdir -p $(OUT)
@@ -87,7 +87,8 @@ asan:
 ASAN_DIR   := $(OBJ)/asan
 ASAN_FLAGS := -std=c++17 -g -O1 -fPIC -fsanitize=address,undefined -fno-sanitize-recover=undefined \
               -fno-omit-frame-pointer -Iinclude -I$(OBJ) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
-ASAN_SRCS  := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp
+ASAN_SRCS  := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp \
+              $(SRC)/hostfeed.cpp
 ASAN_OBJS  := $(patsubst $(SRC)/%,$(ASAN_DIR)/%.o,$(ASAN_SRCS))
 HIP_OBJS   := $(OBJ)/classify.hip.o $(OBJ)/pack.hip.o $(OBJ)/patch.hip.o
 $(ASAN_DIR)/%.o: $(SRC)/% $(HDRS) $(OBJ)/infw_build_id.h

@@ -60,6 +60,7 @@ ALGO_BYTES_PER_PKT = 36  # standard layout: 32 B SoA tuple in + 4 B result word 
 # family-compact layout (infw_batch_soa_c): 4 address bytes per packet + 12 more per IPv6 packet, + 16 B of
 # ifindex/pkt_len/meta/l4word in, + 4 B result word out = 24 + 12 * (IPv6 share) bytes per packet
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PCIE_H2D_GBS = 56.9      # dense pinned H2D copy rate, PCIe Gen5 x16 (tools/micro/pcie.hip, profiles/r06a/pcie.jsonl)
 METRIC = "Mpps classified @1M prefixes x 100 rules, 1/2/4/8 GPUs; % HBM BW roofline"
 
 
@@ -179,11 +180,16 @@ def parse(argv=None):
                     help="with --in-process: every slot on device 0 (rehearsal of the N-slot shape on one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="per-context option (include/infw.h) for every context this bench creates")
-    ap.add_argument("--xdp-ring", choices=("hbm", "host", "registered"), default=None,
+    ap.add_argument("--xdp-ring", choices=("hbm", "host", "registered", "host-packed"), default=None,
                     help="AF_XDP feed: the frames in a umem of 2048-B chunks (--from-frames sets another chunk size) "
                          "in HBM, in pinned host memory (hipHostMalloc) or in the process's own anonymous mapping "
                          "page-locked with infw_host_register (what a daemon's XDP_UMEM_REG memory is), read over "
-                         "PCIe; one RX descriptor ring per interface, classified by infw_classify_xdp (implies --fused)")
+                         "PCIe; one RX descriptor ring per interface, classified by infw_classify_xdp (implies --fused). "
+                         "host-packed: umem and rings in the process's own pageable mapping, read by the library's "
+                         "host packer threads, the packed tuples pipelined through the device "
+                         "(infw_classify_xdp_host); result words into pinned host memory")
+    ap.add_argument("--xdp-chunk", type=int, default=0,
+                    help="with --xdp-ring host-packed: descriptors per pipeline chunk (0: the library's default)")
     ap.add_argument("--fused", action="store_true",
                     help="with --from-frames: one kernel classifies straight from the frames (infw_classify_frames), "
                          "no SoA batch written or read; checked untimed against the packer path's results")
@@ -529,6 +535,21 @@ def run_rank(args):
                 t = own(r[2].numel() * 4).view(torch.int32)
                 t.copy_(r[2].view(-1))
                 r[2] = t
+        elif args.xdp_ring == "host-packed":
+            # the daemon's own pageable memory (an anonymous mapping, huge pages requested as AF_XDP umems commonly
+            # are), never registered: the library's packer threads read it on the CPU; the rings stay pageable too
+            import mmap
+            mm = mmap.mmap(-1, max(frames.numel(), 4096))
+            try:
+                mm.madvise(mmap.MADV_HUGEPAGE)
+            except (AttributeError, OSError):
+                pass
+            umem = torch.from_numpy(np.frombuffer(mm, dtype=np.uint8, count=frames.numel()))
+            umem.copy_(frames)
+            del frames
+            frames = umem
+            host_res = [torch.empty(max(r[1], 1), dtype=torch.int32).pin_memory()[:r[1]] for r in rings]
+            ring_args = [(frames, d, nr, ifv, hr, None) for (ifv, nr, d), hr in zip(rings, host_res)]
         else:
             for r in rings:
                 r[2] = r[2].to(dev)
@@ -537,9 +558,13 @@ def run_rank(args):
         ref = torch.empty_like(results)
         clf.classify_c(batch_c, results=ref)
         off = 0
-        for ifv, nr, d in rings:
-            clf.classify_xdp(frames, d, nr, ifv, results=results[off:off + nr])
-            off += nr
+        if args.xdp_ring == "host-packed":
+            clf.classify_xdp_host(ring_args, chunk=args.xdp_chunk)
+            results.copy_(torch.cat(host_res).to(dev))
+        else:
+            for ifv, nr, d in rings:
+                clf.classify_xdp(frames, d, nr, ifv, results=results[off:off + nr])
+                off += nr
         got = torch.empty_like(results)
         got[perm] = results
         torch.cuda.synchronize()
@@ -554,12 +579,20 @@ def run_rank(args):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
+    step_wall = []
+
     def step(k, ev=None):
         stats = ex.begin(k)
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
-        if args.xdp_ring:
+        if args.xdp_ring == "host-packed":  # synchronous: pack || H2D || classify || D2H inside the library
+            if ev is not None:
+                ev[2].record(stream)
+            t0 = time.perf_counter()
+            clf.classify_xdp_host(ring_args, chunk=args.xdp_chunk)
+            step_wall.append(time.perf_counter() - t0)
+        elif args.xdp_ring:
             if ev is not None:
                 ev[2].record(stream)
             off = 0
@@ -606,7 +639,9 @@ def run_rank(args):
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    if args.from_frames:  # ev[0] -> pack -> ev[2] -> classify -> ev[1]
+    if args.xdp_ring == "host-packed":  # the library's own streams: the step's wall time stands for the kernel's
+        kern_ms = [w * 1e3 for w in step_wall[-args.steps:]]
+    elif args.from_frames:  # ev[0] -> pack -> ev[2] -> classify -> ev[1]
         pack_ms = [e[0].elapsed_time(e[2]) for e in evs]
         kern_ms = [e[2].elapsed_time(e[1]) for e in evs]
     else:
@@ -631,8 +666,26 @@ def run_rank(args):
         assert torch.equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
     digest = stats_digest(digest_block.cpu().numpy())
     # the registry name of the instantiation(s) this line ran (infw_classify_variant: the library's own selector)
-    kernel = clf.variant(infw.INPUT_XDP if args.xdp_ring else {"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
-                                                               "frames": infw.INPUT_FRAMES}[args.layout])
+    kernel = clf.variant(infw.INPUT_COMPACT if args.xdp_ring == "host-packed" else infw.INPUT_XDP if args.xdp_ring else
+                         {"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
+                          "frames": infw.INPUT_FRAMES}[args.layout])
+    host_feed = None
+    if args.xdp_ring == "host-packed":
+        # per step over PCIe: each pipeline chunk of C descriptors carries the family-compact streams without ifindex
+        # (saddr4, pkt_len, meta, l4word: 16 B/packet) and its groups' whole 768-B v6tail blocks; result words back
+        C = ((args.xdp_chunk or (1 << 19)) + 511) // 512 * 512
+        h2d = 0
+        for _, nr, _ in rings:
+            full, rem = divmod(nr, C)
+            h2d += full * 28 * C + ((12 * C + 4 * rem + -(-rem // 64) * 768) if rem else 0)
+        step_s = sum(kern_ms) / len(kern_ms) / 1e3
+        threads = clf.option("host_threads") or min(usable_cores(), 16)
+        host_feed = {"host_threads": threads, "usable_cores": usable_cores(), "chunk": C,
+                     "pcie_h2d_bytes_per_step": h2d, "pcie_h2d_GBps": round(h2d / step_s / 1e9, 2),
+                     "pcie_d2h_GBps": round(4 * n / step_s / 1e9, 2),
+                     "pcie_h2d_bytes_per_packet": round(h2d / max(n, 1), 2),
+                     "pcie_h2d_peak_GBps": PCIE_H2D_GBS, "pcie_h2d_frac": round(h2d / step_s / 1e9 / PCIE_H2D_GBS, 3),
+                     "Mpps_per_host_thread": round(n / step_s / 1e6 / threads, 1)}
     if args.xdp_ring:
         extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "chunk": stride, "rings": len(rings),
                                    "frames_per_ring": [r[1] for r in rings],
@@ -643,7 +696,12 @@ def run_rank(args):
                                        "registered": "the process's own anonymous mapping page-locked with "
                                                      "infw_host_register, read by the kernel over PCIe "
                                                      "(PCIe-inclusive rate)",
-                                       "hbm": "HBM"}[args.xdp_ring]}}
+                                       "host-packed": "the process's own pageable anonymous mapping, read by the "
+                                                      "library's packer threads on the CPU; packed tuples to the "
+                                                      "device and result words back over PCIe (PCIe-inclusive "
+                                                      "rate; kernel_ms_avg is the step's wall time)",
+                                       "hbm": "HBM"}[args.xdp_ring],
+                                   **({"host_feed": host_feed} if host_feed else {})}}
     elif args.fused:
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,
                                       "results_equal_packer_path": fused_check}}
@@ -764,12 +822,14 @@ def run_rank(args):
                       "tables_setup_s": round(v[2], 2), "tables": "imported" if v[3] else "compiled",
                       "host_peak_rss_gib": round(v[4], 2), "packets_per_step": int(v[5])}
                      for r, v in enumerate(per_rank)],
+        # host-packed: the path runs at the host packers' and the link's rate, so its bound is PCIe (the packed
+        # tuples' H2D bytes against the measured dense H2D rate), not HBM
         "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
+            "bound": "pcie" if host_feed else "hbm",
+            "achieved": host_feed["pcie_h2d_GBps"] if host_feed else round(achieved, 2),
+            "peak": PCIE_H2D_GBS if host_feed else HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "frac": host_feed["pcie_h2d_frac"] if host_feed else round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "traffic_from": traffic_from,
             "kernel": kernel,

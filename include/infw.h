@@ -302,6 +302,8 @@ int infw_get_launch(infw_ctx *ctx, int *block, int *scan_group, int *blocks_per_
 /*   stat_flush_tiles 1..1024 (1024): LDS counter flush period in tiles           */
 /*   trace            bit mask to stderr: 1 compile, 2 incremental patch,          */
 /*                    4 commit timing                                              */
+/*   host_threads     0 the CPUs the process may run on (affinity mask, cgroup     */
+/*                    CPU quota; <= 16), or 1..64: infw_classify_xdp_host packers  */
 int infw_set_option(infw_ctx *ctx, const char *name, int64_t value);
 int infw_get_option(infw_ctx *ctx, const char *name, int64_t *value);
 /* Name of option i (0-based), NULL past the last.                             */
@@ -362,8 +364,46 @@ struct infw_xdp_desc {
     uint32_t len;
     uint32_t options;
 };
+/* umem and descs are checked with hipPointerGetAttributes: -EFAULT when either */
+/* is ordinary (pageable, unregistered) host memory, which the GPU cannot read  */
+/* — register such a mapping with infw_host_register first, or use            */
+/* infw_classify_xdp_host, which reads it on the CPU.                          */
 int infw_classify_xdp(infw_ctx *ctx, int dev, const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n,
                       uint32_t ifindex, uint32_t *result_words, uint8_t *xdp_verdicts, void *stream);
+
+/* AF_XDP RX rings over a HOST umem, read by the CPU (the host-fed path): the */
+/* context's packer threads (option host_threads) read each frame's header    */
+/* window where the NIC left it and write the family-compact tuple            */
+/* (infw_batch_soa_c, without the ifindex stream: one ring = one interface)    */
+/* into pinned slots, which go to the device in bulk copies — ~28 B per packet */
+/* over PCIe instead of one 64-B read request per frame.  Pipelined per chunk  */
+/* of `chunk` descriptors (0 = 512K; rounded up to 512): packing of chunk k+1  */
+/* || H2D of k || classify of k-1 || D2H of k-2, chunks running on from one    */
+/* ring into the next.  umem and descs may be any memory the process can read  */
+/* (the socket's mmapped RX ring and umem as they are); results / verdicts are */
+/* host memory (pinned or infw_host_register'ed for the full rate), per ring   */
+/* in descriptor order, either may be NULL.  Frames are read exactly as        */
+/* infw_classify_xdp reads them (same result words, verdicts and counters).    */
+/* Synchronous; the whole call reads one table epoch.  One call at a time per  */
+/* device (concurrent calls queue).                                            */
+struct infw_xdp_ring {
+    const uint8_t *umem;                 /* frame i at umem + (addr & (2^48-1)) + (addr >> 48) */
+    const struct infw_xdp_desc *descs;   /* n RX descriptors                                    */
+    uint64_t n;
+    uint32_t ifindex;                    /* the interface the socket is bound to                 */
+    uint32_t flags;                      /* 0                                                    */
+    uint32_t *results;                   /* n result words, or NULL                              */
+    uint8_t *verdicts;                   /* n XDP verdicts, or NULL                              */
+};
+int infw_classify_xdp_host(infw_ctx *ctx, int dev, const struct infw_xdp_ring *rings, uint32_t n_rings,
+                           uint64_t chunk);
+/* The host packer of infw_classify_xdp_host alone, on the calling thread: one */
+/* ring's frames -> the family-compact streams in host memory (the layout       */
+/* infw_classify_c reads; out->ifindex may be NULL, else it is filled with      */
+/* `ifindex`), for a caller that moves the tuples itself.  Pure host function:  */
+/* no context or device.  Every stream 4-byte aligned.                          */
+int infw_pack_xdp_host(const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n, uint32_t ifindex,
+                       const struct infw_batch_soa_c_out *out);
 
 /* ------------------------------------------------------------------------ */
 /* Sidebands of the data path, opt-in per batch (infw_classify_ex).          */

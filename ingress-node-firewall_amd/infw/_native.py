@@ -95,6 +95,12 @@ class XdpDesc(C.Structure):
     _fields_ = [("addr", C.c_uint64), ("len", C.c_uint32), ("options", C.c_uint32)]
 
 
+class XdpRing(C.Structure):
+    """struct infw_xdp_ring (include/infw.h): one AF_XDP RX ring over a host umem (infw_classify_xdp_host)."""
+    _fields_ = [("umem", C.c_void_p), ("descs", C.c_void_p), ("n", C.c_uint64), ("ifindex", C.c_uint32),
+                ("flags", C.c_uint32), ("results", C.c_void_p), ("verdicts", C.c_void_p)]
+
+
 class EventHdrSt(C.Structure):
     """struct event_hdr_st (ingress_node_firewall.h:58-64), 8 B packed."""
     _pack_ = 1
@@ -148,7 +154,8 @@ ABI_SYMBOLS = [
     "infw_classify_frames_ex",
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
     "infw_table_delete_batch", "infw_set_option", "infw_get_option", "infw_option_name", "infw_classify_variant",
-    "infw_kernel_variant_name", "infw_classify_xdp",
+    "infw_kernel_variant_name", "infw_classify_xdp", "infw_classify_xdp_host",
+    "infw_pack_xdp_host",
 ]
 ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
 INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES, INPUT_XDP = 0, 1, 2, 3  # INFW_INPUT_*
@@ -233,6 +240,8 @@ _sig = {
     "infw_kernel_variant_name": (C.c_char_p, [C.c_int]),
     "infw_classify_xdp": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                     C.c_void_p, C.c_void_p, C.c_void_p]),
+    "infw_classify_xdp_host": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64]),
+    "infw_pack_xdp_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, P(BatchSoaC)]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -299,7 +308,7 @@ for _name, (_res, _args) in _wsig.items():
     _f.restype = _res
     _f.argtypes = _args
 
-assert C.sizeof(EventHdrSt) == 8 and C.sizeof(EventRec) == 24
+assert C.sizeof(EventHdrSt) == 8 and C.sizeof(EventRec) == 24 and C.sizeof(XdpRing) == 48
 if lib.infw_abi_version() != ABI_VERSION:
     raise ImportError(f"{LIB_PATH}: ABI {lib.infw_abi_version()}, these bindings are ABI {ABI_VERSION}: rebuild (make)")
 

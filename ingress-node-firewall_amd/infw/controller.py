@@ -158,7 +158,7 @@ class Statistics:
         self.failed_lookups = 0
         for rule in range(1, self.MAX_INGRESS_RULES):        # statistics.go:126
             try:
-                slots = self.c.stats_read(rule)
+                slots = self.c.stats_read(rule, wait=False)  # a snapshot beside running batches, as XDP runs on
             except InfwError:                                # statistics.go:127-130: logged, next rule
                 self.failed_lookups += 1
                 continue

@@ -50,6 +50,7 @@ class Classifier:
         arr = (C.c_int * len(devices))(*devices) if devices else None
         check(N.lib.infw_create(C.byref(self._ctx), arr, len(devices) if devices else 0, max_entries, flags),
               "infw_create")
+        self._devices = list(devices) if devices else None
         for k, v in {**DEFAULT_OPTIONS, **(options or {})}.items():
             self.set_option(k, v)
 
@@ -341,6 +342,19 @@ class Classifier:
                                       results.data_ptr() if results is not None else None,
                                       verdicts.data_ptr() if verdicts is not None else None, sp), "classify_xdp")
 
+    def classify_xdp_host(self, rings, chunk: int = 0, dev: int = 0) -> None:
+        """infw_classify_xdp_host: AF_XDP RX rings over a host umem, packed on the context's host threads and
+        classified through the device (synchronous).  `rings`: (umem, descs, n, ifindex, results, verdicts) per
+        ring — host buffers as torch CPU tensors, numpy arrays or raw addresses; results / verdicts may be None."""
+        def ptr(x):
+            if x is None or isinstance(x, int):
+                return x
+            return x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data
+        arr = (N.XdpRing * max(1, len(rings)))()
+        for i, (umem, descs, n, ifindex, results, verdicts) in enumerate(rings):
+            arr[i] = N.XdpRing(ptr(umem), ptr(descs), n, ifindex, 0, ptr(results), ptr(verdicts))
+        check(N.lib.infw_classify_xdp_host(self._ctx, dev, arr, len(rings), chunk), "classify_xdp_host")
+
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
         """The perf samples of the deny events classify_events wrote (kernel.c:392-399) from the frames the batch was
@@ -368,15 +382,29 @@ class Classifier:
         return b.value, g.value, p.value
 
     # -- statistics map
-    def stats_read(self, rule_id: int) -> List[RuleStatisticsSt]:
-        """Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt): one entry per device slot."""
+    def _settle(self) -> None:
+        """Wait for the work queued on this context's devices (torch streams included): the C readers take a
+        snapshot without waiting for anything, like a per-CPU map read beside running XDP programs."""
+        if self.num_devices:
+            import torch
+            for d in sorted(set(self._devices or [torch.cuda.current_device()])):
+                torch.cuda.synchronize(d)
+
+    def stats_read(self, rule_id: int, wait: bool = True) -> List[RuleStatisticsSt]:
+        """Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt): one entry per device slot.  wait=False: the snapshot
+        as the counters stand (what a poller beside running batches sees); True: after this process's queued work."""
+        if wait:
+            self._settle()
         nd = max(1, self.num_devices)
         arr = (RuleStatisticsSt * nd)()
         ns = C.c_int(0)
         check(N.lib.infw_stats_read(self._ctx, rule_id, arr, C.byref(ns)), "stats_read")
         return list(arr[: ns.value])
 
-    def stats_read_all(self) -> np.ndarray:
+    def stats_read_all(self, wait: bool = True) -> np.ndarray:
+        """All 1024 rules summed over slots (infw_stats_read_all); wait as for stats_read."""
+        if wait:
+            self._settle()
         arr = (RuleStatisticsSt * N.MAX_TARGETS)()
         check(N.lib.infw_stats_read_all(self._ctx, arr), "stats_read_all")
         return np.frombuffer(bytes(arr), dtype=np.uint64).reshape(N.MAX_TARGETS, 4).copy()
@@ -436,6 +464,36 @@ class HostSoa:
 
     def arrays(self):
         return (self.saddr, self.ifindex, self.pkt_len, self.meta, self.l4word)
+
+
+def pack_xdp_host(umem: np.ndarray, descs: np.ndarray, ifindex: int) -> Dict[str, np.ndarray]:
+    """infw_pack_xdp_host: the host packer of infw_classify_xdp_host on the calling thread — one AF_XDP ring's frames
+    (`descs`: n x 16 B struct xdp_desc over the bytes of `umem`) -> the family-compact streams (numpy, host)."""
+    descs = np.ascontiguousarray(descs).view(np.uint8).reshape(-1, 16)
+    n = descs.shape[0]
+    out = {k: np.zeros(max(n, 1), np.uint32) for k in ("saddr4", "ifindex", "pkt_len", "meta", "l4word")}
+    out["v6tail"] = np.zeros(max(1, (n + 63) // 64) * 768, np.uint8)
+    o = N.BatchSoaC(*(out[k].ctypes.data for k in ("saddr4", "v6tail", "ifindex", "pkt_len", "meta", "l4word")))
+    umem = np.ascontiguousarray(umem)
+    check(N.lib.infw_pack_xdp_host(umem.ctypes.data, descs.ctypes.data, n, ifindex, C.byref(o)), "pack_xdp_host")
+    return {k: v[:n] if k != "v6tail" else v for k, v in out.items()}
+
+
+def compact_to_tuples(c: Dict[str, np.ndarray]) -> np.ndarray:
+    """Family-compact streams -> n x 8 u32 tuples {saddr[4], ifindex, pkt_len, meta, l4word} (infw_debug_walk's input;
+    the inverse of the compact layout: a group's IPv6 packets take its tail slots in packet order)."""
+    n = c["meta"].shape[0]
+    t = np.zeros((n, 8), np.uint32)
+    t[:, 0] = c["saddr4"]
+    tails = c["v6tail"].view(np.uint32)
+    is6 = (c["meta"] & 0xFFFF) == 0x86DD
+    for g in range(0, n, 64):
+        idx = np.nonzero(is6[g:g + 64])[0] + g
+        base = g // 64 * 192
+        for r, i in enumerate(idx):
+            t[i, 1:4] = tails[base + 3 * r: base + 3 * r + 3]
+    t[:, 4], t[:, 5], t[:, 6], t[:, 7] = c["ifindex"], c["pkt_len"], c["meta"], c["l4word"]
+    return t
 
 
 def verdicts_from_results(results: np.ndarray, meta: np.ndarray) -> np.ndarray:

@@ -1,0 +1,175 @@
+"""The host-fed AF_XDP path (infw_classify_xdp_host): RX rings over a umem in ordinary (pageable) host memory, read by
+the context's packer threads, the packed tuples pipelined through the device in chunks.
+
+One ring per interface (a socket is bound to one interface queue), rings of ragged sizes (empty, one frame, a partial
+group, several chunks plus a partial one) so that chunks run from one ring into the next and the host slots are
+reused many times; aligned and unaligned descriptor modes.  Result words, verdicts and per-rule counters must equal
+the oracle's on the same frames (oracle/infw_oracle.c from the frame bytes), and equal infw_classify_xdp's — the
+kernel reading the same rings in place — when the memory is registered."""
+import mmap
+
+import numpy as np
+import pytest
+import torch
+
+import infw
+from infw import workloads as W
+
+from parity import oracle_for
+from test_hostpack_cpu import ring
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.fixture(scope="module")
+def setup():
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=50000, n_templates=256)
+    clf = infw.Classifier(devices=[0], max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    return wl, clf, oracle_for(wl)
+
+
+def rings_of(wl, start, sizes, mode, seed):
+    """Frames of packets [start, ...) split by interface into rings of the given sizes (one ifindex per ring)."""
+    rng = np.random.default_rng(seed)
+    hdr, cap, pl, ifx = wl.frames(start, 4 * sum(sizes) + 4096)
+    out, used = [], np.zeros(hdr.shape[0], bool)
+    for r, size in enumerate(sizes):
+        v = np.unique(ifx)[r % len(np.unique(ifx))]
+        idx = np.nonzero((ifx == v) & ~used)[0][:size]
+        assert idx.size == size
+        used[idx] = True
+        umem, desc = ring(hdr[idx], pl[idx], mode, rng)
+        out.append(dict(ifindex=int(v), hdr=hdr[idx], pl=pl[idx], umem=umem, desc=desc))
+    return out
+
+
+def oracle_of(m, rings):
+    """Per-ring expected result words and verdicts, and the counters of all rings together."""
+    hdr = np.concatenate([r["hdr"] for r in rings])
+    pl = np.concatenate([r["pl"] for r in rings])
+    ifx = np.concatenate([np.full(r["pl"].size, r["ifindex"], np.uint32) for r in rings])
+    want, wver, wst, _ = m.classify_frames(hdr, pl, pl, ifx, nthreads=8)
+    cut = np.cumsum([0] + [r["pl"].size for r in rings])
+    return [want[a:b] for a, b in zip(cut, cut[1:])], [wver[a:b] for a, b in zip(cut, cut[1:])], wst
+
+
+def run_host(clf, rings, chunk, pinned_out=False):
+    res, ver, args = [], [], []
+    for r in rings:
+        n = r["pl"].size
+        if pinned_out:
+            rr = torch.full((max(n, 1),), -1, dtype=torch.int32).pin_memory()
+            vv = torch.full((max(n, 1),), 7, dtype=torch.uint8).pin_memory()
+        else:  # ordinary pageable host memory
+            rr, vv = torch.full((max(n, 1),), -1, dtype=torch.int32), torch.full((max(n, 1),), 7, dtype=torch.uint8)
+        res.append(rr)
+        ver.append(vv)
+        args.append((r["umem"], r["desc"], n, r["ifindex"], rr, vv))
+    clf.stats_reset()
+    clf.classify_xdp_host(args, chunk=chunk)
+    return [x[:r["pl"].size].numpy().view(np.uint32) for x, r in zip(res, rings)], \
+        [x[:r["pl"].size].numpy() for x, r in zip(ver, rings)], clf.stats_read_all()
+
+
+@pytest.mark.parametrize("mode", ["aligned", "unaligned"])
+@pytest.mark.parametrize("chunk", [512, 0])
+def test_xdp_host_matches_oracle(setup, mode, chunk):
+    wl, clf, m = setup
+    sizes = [0, 1, 29, 3 * 512 + 64 + 17, 40000 + 3, 1200]
+    rings = rings_of(wl, 1000 + chunk, sizes, mode, seed=7 + chunk)
+    want, wver, wst = oracle_of(m, rings)
+    got, gver, gst = run_host(clf, rings, chunk, pinned_out=(chunk == 0))
+    for i, (g, w) in enumerate(zip(got, want)):
+        bad = np.nonzero(g != w)[0]
+        assert bad.size == 0, (mode, chunk, i, bad[:5], g[bad[:5]], w[bad[:5]])
+        assert np.array_equal(gver[i], wver[i]), (mode, chunk, i)
+    assert np.array_equal(gst, wst)
+    both = np.concatenate(want)
+    assert (both & 0xFF).astype(bool).mean() > 0.3 and len({r["ifindex"] for r in rings}) > 1
+
+
+def test_xdp_host_threads_and_chunks_agree(setup):
+    """Any packer thread count and chunk size gives the same words and counters (the split of a chunk among the
+    threads and the slot reuse are invisible)."""
+    wl, clf, m = setup
+    rings = rings_of(wl, 50000, [70001, 333], "aligned", seed=9)
+    want, _, wst = oracle_of(m, rings)
+    try:
+        for threads, chunk in ((1, 4096), (3, 1024), (16, 512), (0, 0)):
+            clf.set_option("host_threads", threads)
+            got, _, gst = run_host(clf, rings, chunk)
+            assert all(np.array_equal(g, w) for g, w in zip(got, want)), (threads, chunk)
+            assert np.array_equal(gst, wst), (threads, chunk)
+    finally:
+        clf.set_option("host_threads", 0)
+
+
+def test_xdp_host_equals_device_read(setup):
+    """The same rings in registered memory: infw_classify_xdp (the kernel reading umem and ring over PCIe) and
+    infw_classify_xdp_host give identical result words and counters."""
+    wl, clf, m = setup
+    rings = rings_of(wl, 90000, [5000, 7777], "unaligned", seed=11)
+    got, _, gst = run_host(clf, rings, 0)
+    clf.stats_reset()
+    dres = []
+    for r in rings:
+        u = torch.from_numpy(r["umem"]).pin_memory()
+        d = torch.from_numpy(r["desc"].view(np.int32)).pin_memory()
+        out = torch.empty(r["pl"].size, dtype=torch.int32, device="cuda:0")
+        clf.classify_xdp(u, d, r["pl"].size, r["ifindex"], results=out)
+        torch.cuda.synchronize()
+        dres.append(out.cpu().numpy().view(np.uint32))
+    assert all(np.array_equal(g, d) for g, d in zip(got, dres))
+    assert np.array_equal(clf.stats_read_all(), gst)
+
+
+def test_xdp_device_read_rejects_pageable(setup):
+    """infw_classify_xdp on pageable memory (a socket's mmapped ring as it is) returns -EFAULT instead of faulting
+    the GPU; registered with infw_host_register, the same memory classifies."""
+    wl, clf, _ = setup
+    r = rings_of(wl, 123, [300], "aligned", seed=13)[0]
+    maps, arrs = [], []
+    for a in (r["umem"], r["desc"]):  # the process's own anonymous mappings (page-aligned), as a daemon's
+        mm = mmap.mmap(-1, max(a.nbytes, 4096))
+        b = np.frombuffer(mm, dtype=a.dtype, count=a.size).reshape(a.shape)
+        b[...] = a
+        maps.append(mm)
+        arrs.append(b)
+    u, d = torch.from_numpy(arrs[0]), torch.from_numpy(arrs[1].view(np.int32))  # pageable CPU tensors
+    out = torch.empty(300, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(infw.InfwError) as e:
+        clf.classify_xdp(u, d, 300, r["ifindex"], results=out)
+    assert e.value.errno == 14
+    for b in arrs:
+        clf.host_register(b)
+    try:
+        clf.classify_xdp(u, d, 300, r["ifindex"], results=out)
+        torch.cuda.synchronize()
+        ref, _, _ = run_host(clf, [r], 0)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref[0])
+    finally:
+        for b in arrs:
+            clf.host_unregister(b)
+        del u, d, b, arrs
+
+
+def test_xdp_host_rejects_bad_rings(setup):
+    _, clf, _ = setup
+    from infw import _native as N
+    arr = (N.XdpRing * 1)()
+    arr[0] = N.XdpRing(None, None, 5, 1, 0, None, None)  # frames but no umem
+    assert N.lib.infw_classify_xdp_host(clf._ctx, 0, arr, 1, 0) == -22
+    u = np.zeros(4096, np.uint8)
+    d = np.zeros((1, 4), np.uint32)
+    arr[0] = N.XdpRing(u.ctypes.data, d.ctypes.data, 1, 1, 1, None, None)  # flags != 0
+    assert N.lib.infw_classify_xdp_host(clf._ctx, 0, arr, 1, 0) == -22
+    assert N.lib.infw_classify_xdp_host(clf._ctx, 0, arr, 0, 0) == 0  # no rings: nothing to do
+    assert N.lib.infw_classify_xdp_host(clf._ctx, 5, arr, 1, 0) == -22  # no such device slot

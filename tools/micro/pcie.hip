@@ -109,5 +109,59 @@ int main() {
         }
     }
     CHECK(hipDeviceSynchronize());
+    // The copy engines instead of the compute units (SDMA): hipMemcpy2DAsync gathering each chunk's 64-B header window
+    // (width 64 at pitch 2048) from pinned host memory into a dense HBM array — the one-copy-per-batch alternative to
+    // the classify kernel reading windows in place — on 1, 2 and 4 streams (each stream's copies go to one engine),
+    // beside dense H2D / D2H copies of the same bytes for the link's bulk rate.
+    {
+        uint8_t *dense = nullptr;
+        CHECK(hipMalloc(&dense, frames * 64));
+        hipStream_t st[4];
+        for (auto &s : st) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        auto timed = [&](int ns, int kind) -> double {  // kind 0: 2D gather, 1: dense H2D, 2: dense D2H
+            double best = 1e30;
+            for (int rep = 0; rep < 4; rep++) {
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipEventRecord(a, st[0]));
+                for (int s = 1; s < ns; s++) CHECK(hipStreamWaitEvent(st[s], a, 0));
+                const uint64_t per = frames / ns;
+                for (int s = 0; s < ns; s++) {
+                    const uint64_t f0 = s * per;
+                    if (kind == 0)
+                        CHECK(hipMemcpy2DAsync(dense + f0 * 64, 64, host + f0 * stride, stride, 64, per,
+                                               hipMemcpyHostToDevice, st[s]));
+                    else if (kind == 1)
+                        CHECK(hipMemcpyAsync(dense + f0 * 64, host + f0 * 64, per * 64, hipMemcpyHostToDevice, st[s]));
+                    else
+                        CHECK(hipMemcpyAsync(host + f0 * 64, dense + f0 * 64, per * 64, hipMemcpyDeviceToHost, st[s]));
+                }
+                for (int s = 1; s < ns; s++) {
+                    hipEvent_t e;
+                    CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    CHECK(hipEventRecord(e, st[s]));
+                    CHECK(hipStreamWaitEvent(st[0], e, 0));
+                    CHECK(hipEventDestroy(e));
+                }
+                CHECK(hipEventRecord(b, st[0]));
+                CHECK(hipEventSynchronize(b));
+                float ms = 0;
+                CHECK(hipEventElapsedTime(&ms, a, b));
+                if (ms < best) best = ms;
+            }
+            return best;
+        };
+        for (int ns : {1, 2, 4}) {
+            const double g = timed(ns, 0), h = timed(ns, 1), d = timed(ns, 2);
+            printf("{\"sdma_streams\": %d, \"gather2d_Mwindows_s\": %.1f, \"gather2d_GBps\": %.2f, "
+                   "\"dense_h2d_GBps\": %.1f, \"dense_d2h_GBps\": %.1f, \"frames\": %llu}\n",
+                   ns, frames / g / 1e3, frames * 64 / g / 1e6, frames * 64 / h / 1e6, frames * 64 / d / 1e6,
+                   (unsigned long long)frames);
+            fflush(stdout);
+        }
+        CHECK(hipFree(dense));
+    }
     return 0;
 }
