@@ -188,6 +188,10 @@ def parse(argv=None):
                          "host-packed: umem and rings in the process's own pageable mapping, read by the library's "
                          "host packer threads, the packed tuples pipelined through the device "
                          "(infw_classify_xdp_host); result words into pinned host memory")
+    ap.add_argument("--umem-order", choices=("packet", "ring"), default=None,
+                    help="AF_XDP umem layout: frames at their packet index (rings interleave: default for hbm/host/"
+                         "registered) or each ring's frames back to back in arrival order (a socket's own umem fed by a "
+                         "FIFO fill ring: default for host-packed)")
     ap.add_argument("--xdp-chunk", type=int, default=0,
                     help="with --xdp-ring host-packed: descriptors per pipeline chunk (0: the library's default)")
     ap.add_argument("--fused", action="store_true",
@@ -197,6 +201,7 @@ def parse(argv=None):
     if args.xdp_ring:
         args.from_frames = args.from_frames or 2048
         args.fused = True
+        args.umem_order = args.umem_order or ("ring" if args.xdp_ring == "host-packed" else "packet")
         if args.batch == 1 << 27:
             args.batch = 1 << 24  # 16M frames x 2048 B = 32 GiB of umem
     args.options = {}
@@ -501,15 +506,23 @@ def run_rank(args):
         ifx_h = f_ifx[:n].cpu().numpy().view(np.uint32)
         lin_h = f_lin[:n].cpu().numpy().view(np.uint32)
         len_h = np.where(lin_h < 80, lin_h, f_len[:n].cpu().numpy().view(np.uint32))
-        order = []
+        # umem order: "packet" — every frame at its packet index (the interfaces' rings interleave in one umem, so a
+        # ring's addresses ascend with gaps); "ring" — each ring's frames back to back in arrival order, as a socket's
+        # own umem holds them in steady state when its fill ring returns chunks in the order they were consumed
+        order, at = [], 0
         for ifv in np.unique(ifx_h):
             idx = np.nonzero(ifx_h == ifv)[0]
             d = np.zeros((len(idx), 4), np.uint32)
-            a = idx.astype(np.uint64) * np.uint64(stride)
+            slots = idx.astype(np.uint64) if args.umem_order == "packet" else np.arange(at, at + len(idx), dtype=np.uint64)
+            a = slots * np.uint64(stride)
             d[:, 0], d[:, 1], d[:, 2] = a & np.uint64(0xFFFFFFFF), a >> np.uint64(32), len_h[idx]
             rings.append([int(ifv), len(idx), torch.from_numpy(d.view(np.int32))])
             order.append(idx)
+            at += len(idx)
         perm = torch.from_numpy(np.concatenate(order)).to(dev)
+        if args.umem_order == "ring":  # frame k of the umem = packet perm[k]
+            frames = frames.view(-1, stride)[:n][perm].reshape(-1)
+            torch.cuda.synchronize()
         if args.xdp_ring == "host":  # umem and rings in pinned host memory: the kernel reads them over PCIe
             umem = torch.empty(frames.numel(), dtype=torch.uint8, pin_memory=True)
             umem.copy_(frames)
@@ -539,7 +552,8 @@ def run_rank(args):
             # the daemon's own pageable memory (an anonymous mapping, huge pages requested as AF_XDP umems commonly
             # are), never registered: the library's packer threads read it on the CPU; the rings stay pageable too
             import mmap
-            mm = mmap.mmap(-1, max(frames.numel(), 4096))
+            # private (not shared) anonymous memory: transparent huge pages apply to it, as to a daemon's umem
+            mm = mmap.mmap(-1, max(frames.numel(), 4096), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
             try:
                 mm.madvise(mmap.MADV_HUGEPAGE)
             except (AttributeError, OSError):
@@ -687,7 +701,8 @@ def run_rank(args):
                      "pcie_h2d_peak_GBps": PCIE_H2D_GBS, "pcie_h2d_frac": round(h2d / step_s / 1e9 / PCIE_H2D_GBS, 3),
                      "Mpps_per_host_thread": round(n / step_s / 1e6 / threads, 1)}
     if args.xdp_ring:
-        extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "chunk": stride, "rings": len(rings),
+        extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "umem_order": args.umem_order, "chunk": stride,
+                                   "rings": len(rings),
                                    "frames_per_ring": [r[1] for r in rings],
                                    "results_equal_packer_path": fused_check,
                                    "note": "umem and descriptor rings in " + {

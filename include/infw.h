@@ -301,7 +301,7 @@ int infw_get_launch(infw_ctx *ctx, int *block, int *scan_group, int *blocks_per_
 /*   split_min_mb     0..1048576 (1024): auto splits past this many MiB of lines  */
 /*   stat_flush_tiles 1..1024 (1024): LDS counter flush period in tiles           */
 /*   trace            bit mask to stderr: 1 compile, 2 incremental patch,          */
-/*                    4 commit timing                                              */
+/*                    4 commit timing, 8 infw_classify_xdp_host pipeline timing    */
 /*   host_threads     0 the CPUs the process may run on (affinity mask, cgroup     */
 /*                    CPU quota; <= 16), or 1..64: infw_classify_xdp_host packers  */
 int infw_set_option(infw_ctx *ctx, const char *name, int64_t value);
@@ -325,6 +325,11 @@ int infw_classify_variant(infw_ctx *ctx, int dev, int input, uint32_t flags, cha
 /* Registry of every kernel instantiation the library launches: name of entry */
 /* i (0-based), NULL past the last.                                            */
 const char *infw_kernel_variant_name(int i);
+/* Launch counters of device slot `dev` since infw_create: counts[0] two-phase */
+/* launches (phase 1 + decide), counts[1] launches the selector made two-phase */
+/* that ran the fused kernel because the scratch could not be allocated (no    */
+/* pool, or the pool out of memory) — results are the same either way.        */
+int infw_launch_counts(infw_ctx *ctx, int dev, uint64_t counts[2]);
 
 /* Frame headers -> SoA tuples on the device (the packer of the batch format  */
 /* above, run as a kernel over frames already in HBM).  Asynchronous.          */
@@ -485,6 +490,21 @@ int infw_host_unregister(infw_ctx *ctx, void *ptr);
 /* Statistics — ingress_node_firewall_statistics_map (kernel.c:36-41,        */
 /* PERCPU_ARRAY[1024] of ruleStatistics_st).  One slot per device plays the  */
 /* role of one per-CPU slot; readers sum slots like statistics.go:126-157.   */
+/*                                                                          */
+/* Where the multi-GPU sum happens — the library never runs a collective:   */
+/*  - one process, one context over N devices (the node daemon's shape):    */
+/*    each device slot counts its own batches; infw_stats_read returns the  */
+/*    N per-slot values (the []BpfRuleStatisticsSt of one per-CPU lookup)   */
+/*    and the caller sums them, as statistics.go:132-156 does;              */
+/*    infw_stats_read_all returns that sum (u64 wrap-around) for all rules; */
+/*  - one process per GPU (torch.distributed / RCCL ranks): each rank's     */
+/*    context has one slot; a caller that wants node totals binds the slot  */
+/*    to its own device buffer (infw_stats_bind) and all-reduces it with    */
+/*    its communicator (bench.py: an async RCCL all-reduce), or reads each  */
+/*    rank's slot and sums on the host — the per-CPU sum again.             */
+/* Reads are snapshots: a lookup copies the slot on a stream of its own and  */
+/* waits for nothing queued on other streams (batches in flight keep adding,*/
+/* like XDP on other CPUs while statistics.go polls).                       */
 /* ------------------------------------------------------------------------ */
 /* Map.Lookup(uint32(rule), &[]BpfRuleStatisticsSt)  statistics.go:127       */
 /* per_slot must hold infw_num_devices() entries; -ENOENT for rule >= 1024.   */

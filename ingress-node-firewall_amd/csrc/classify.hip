@@ -1218,6 +1218,7 @@ extern "C" int infw_launch_classify(const infw_launch_args *a) {
     const Variant *v = find_variant(k);
     if (v && k.split) {
         const int rc = launch_split(*a, *v, bi, st);
+        if (a->split_counts && rc >= 0) __atomic_fetch_add(&a->split_counts[rc == 0 ? 0 : 1], 1, __ATOMIC_RELAXED);
         if (rc <= 0) return rc;
         k = select_variant(*a, false, &bpc);  // no scratch: the fused kernel
         v = find_variant(k);

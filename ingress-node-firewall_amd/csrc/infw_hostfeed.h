@@ -2,15 +2,19 @@
 //
 // A pool of worker threads packs a call's chunks (each a run of one AF_XDP ring's descriptors) into a ring of pinned
 // host slots, in chunk order, while the calling thread — the coordinator — moves packed chunks through the device
-// (H2D, classify, D2H on three HIP streams).  Every worker owns the same share of every chunk and runs through the
-// chunks without a barrier: chunk k counts as packed when its last share is done (shares finish in chunk order, so
-// packed() only grows), and a worker may start chunk k once the coordinator has released it (its slot's previous
-// chunk has left for the device).  Waits spin briefly and then sleep on a condition variable.
+// (H2D, classify, D2H on three HIP streams).  Work is handed out dynamically: every chunk is cut into units of
+// kPackUnit descriptors (whole INFW_V6_GROUP groups), numbered across the call, and a worker claims the next unit
+// with one atomic increment — a worker that is descheduled or slower (an SMT sibling, a remote NUMA node) delays one
+// unit, not a fixed share of every chunk.  A worker may pack a unit of chunk k once the coordinator has released k
+// (its slot's previous chunk has left for the device); chunk k counts as packed when all of its units are done and
+// so are all earlier chunks (the packed frontier only grows).  Waits spin briefly and then sleep on a condition
+// variable.
 #pragma once
 #include <stdint.h>
 
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -39,6 +43,8 @@ struct XdpChunk {
     uint32_t ifindex;
 };
 
+constexpr uint64_t kPackUnit = 4096;  // descriptors per claimed unit (~30 us of one core's packing)
+
 class HostPackPool {
    public:
     explicit HostPackPool(int threads);
@@ -51,21 +57,31 @@ class HostPackPool {
     void release(uint64_t upto) { released_.set(base_ + upto); }           // chunks < upto may be packed
     // Stop (abort: chunks not yet started are skipped) and wait until no worker touches the job.
     void end(bool abort);
+    // Worker time since the last begin(), summed over the workers (ns): packing, and waiting for a chunk's release
+    // (its host slot still on its way to the device) — read after end()
+    uint64_t pack_ns() const { return pack_ns_.load(); }
+    uint64_t release_wait_ns() const { return release_wait_ns_.load(); }
 
    private:
-    void work(int t);
+    void work();
+    void advance_frontier();
     std::vector<std::thread> workers_;
     Signal job_;       // generation of the current job (workers wait for the next one)
     Signal released_;  // base_ + chunks released
-    Signal packed_;    // base_ + chunks fully packed
+    Signal packed_;    // base_ + chunks fully packed (the frontier)
     Signal idle_;      // workers that finished the current job (cumulative)
-    std::vector<std::atomic<int>> shares_done_;  // per slot (at most 8): shares of its chunks done in this job
+    std::vector<uint64_t> unit_base_;                // first unit of chunk k; back() = units of the job
+    std::unique_ptr<std::atomic<uint32_t>[]> done_;  // units of chunk k done
+    std::atomic<uint64_t> next_unit_{0};
+    std::mutex frontier_mu_;
+    uint64_t frontier_ = 0;  // chunks < frontier_ are packed (under frontier_mu_)
     const std::vector<XdpChunk> *chunks_ = nullptr;
     std::vector<infw_hostpack_out> slots_;
     uint64_t base_ = 0;  // chunk sequence number of the job's chunk 0 (the signals only grow)
     uint64_t gen_ = 0;
     std::atomic<bool> abort_{false}, quit_{false};
     std::atomic<uint64_t> idle_total_{0};
+    std::atomic<uint64_t> pack_ns_{0}, release_wait_ns_{0};
     int n_threads_;
 };
 

@@ -254,7 +254,8 @@ struct Options {
     int32_t split = -1;             // two-phase classify: -1 when the entry lines exceed split_min_mb, 0 never, 1 always
     int64_t split_min_mb = 1024;
     int32_t stat_flush_tiles = 1024; // a workgroup flushes its LDS counters every this many tiles (1..1024)
-    int32_t trace = 0;              // stderr: 1 compile phases, 2 incremental patch phases, 4 commit timing
+    int32_t trace = 0;              // stderr: 1 compile phases, 2 incremental patch phases, 4 commit timing,
+                                    // 8 classify_xdp_host pipeline timing
     int32_t host_threads = 0;       // packer threads of infw_classify_xdp_host: 0 = the CPUs the process may use (<= 16)
 };
 // Name, bounds and field of every option (abi.cpp infw_set_option / infw_get_option / infw_option_name).

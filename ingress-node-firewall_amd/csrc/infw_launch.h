@@ -30,6 +30,8 @@ struct infw_launch_args {
     int block, group, blocks_per_cu;  // a shape infw_launch_shape_ok accepts
     hipStream_t stream;
     hipMemPool_t pool;             // the context's pool for the two-phase scratch (null: the fused kernel runs)
+    uint64_t *split_counts;        // non-null: [0] += 1 per two-phase launch, [1] += 1 per two-phase launch that ran
+                                   // the fused kernel for want of scratch (host-side atomics; infw_launch_counts)
     infw_event_rec *ev;
     uint64_t ev_cap;
     uint64_t *ev_count;            // non-null: the deny-event sideband

@@ -70,6 +70,13 @@ class Classifier:
               "classify_variant")
         return buf.value.decode()
 
+    def launch_counts(self, dev: int = 0) -> tuple:
+        """(two-phase launches, two-phase launches run as the fused kernel for want of scratch) since creation
+        (infw_launch_counts)."""
+        c = (C.c_uint64 * 2)()
+        check(N.lib.infw_launch_counts(self._ctx, dev, c), "launch_counts")
+        return int(c[0]), int(c[1])
+
     # -- lifecycle
     def close(self):
         if self._ctx:

@@ -75,6 +75,7 @@ def test_every_registered_variant_matches_the_oracle():
             ver.fill_(7)
             events_count.zero_()
             evs = dict(events=events, events_count=events_count) if ev else {}
+            split_before = clf.launch_counts()
             if inp == "soa":
                 if ev:
                     clf.classify_events(batch, events, events_count, results=res, verdicts=ver)
@@ -89,6 +90,9 @@ def test_every_registered_variant_matches_the_oracle():
                                     **evs)
             torch.cuda.synchronize()
             label = f"{name} ({kind}, split={split}, shape={shape}, {inp}, ev={ev}, dbg={dbg})"
+            # the launch really took the form the name says (a two-phase launch without scratch would run fused)
+            taken, fell_back = (a - b for a, b in zip(clf.launch_counts(), split_before))
+            assert (taken, fell_back) == ((1, 0) if "+decide" in name else (0, 0)), (label, taken, fell_back)
             wres, wver, wstats = (xres, xver, xstats) if inp == "xdp" else (ores, over, ostats)
             gres = res.cpu().numpy().view(np.uint32)
             bad = np.nonzero(gres != wres)[0]

@@ -95,12 +95,14 @@ def test_options_validated():
     c = infw.Classifier(flags=infw.F_HOST_ONLY)
     names = infw.option_names()
     assert names == ["short_table", "d16", "dt_half", "dt_parts", "dt_adapt", "dt_budget_mb", "compile_threads",
-                     "split", "split_min_mb", "stat_flush_tiles", "trace"]
+                     "split", "split_min_mb", "stat_flush_tiles", "trace", "host_threads"]
     defaults = {n: c.option(n) for n in names}
     assert defaults == {"short_table": -1, "d16": -1, "dt_half": -1, "dt_parts": 0, "dt_adapt": 1, "dt_budget_mb": 2048,
-                        "compile_threads": 0, "split": -1, "split_min_mb": 1024, "stat_flush_tiles": 1024, "trace": 0}
+                        "compile_threads": 0, "split": -1, "split_min_mb": 1024, "stat_flush_tiles": 1024, "trace": 0,
+                        "host_threads": 0}
     for name, bad in [("nope", 0), ("dt_parts", 3), ("dt_parts", 32), ("split", 2), ("short_table", 2),
-                      ("stat_flush_tiles", 0), ("stat_flush_tiles", 1025), ("dt_budget_mb", 1), ("trace", 8)]:
+                      ("stat_flush_tiles", 0), ("stat_flush_tiles", 1025), ("dt_budget_mb", 1), ("trace", 16),
+                      ("host_threads", -1), ("host_threads", 65)]:
         with pytest.raises(infw.InfwError) as e:
             c.set_option(name, bad)
         assert e.value.errno == 22

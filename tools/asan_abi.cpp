@@ -309,7 +309,7 @@ static int selftest() {
         CHECK(infw_set_option(o.c, "dt_parts", 8) == 0 && infw_get_option(o.c, "dt_parts", &v) == 0 && v == 8);
         int n_opt = 0;
         for (; infw_option_name(n_opt); n_opt++) CHECK(infw_get_option(o.c, infw_option_name(n_opt), &v) == 0);
-        CHECK(n_opt == 11);
+        CHECK(n_opt == 12);
         char name[256];
         CHECK(infw_classify_variant(o.c, 0, INFW_INPUT_SOA, 0, name, sizeof name) == 0);
         CHECK(infw_classify_variant(o.c, 0, INFW_INPUT_SOA, 0, name, 4) == -ERANGE);

@@ -3,13 +3,14 @@
 #   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_pass.sh <tag> <step> [<step> ...]
 # steps (in the order given; the pass stops at the first failing step, and no GPU step follows a fault or timeout):
 #   suite        pytest -m gpu (as the driver runs it, with per-test timeouts) and __graft_entry__.smoke()
-#   test:<expr>  pytest -m gpu -k <expr> (one test group)
+#   test:<a,b>   pytest -m gpu -k "a or b" (one test group)
 #   bench        the default bench line (what the driver's BENCH record runs)
 #   lines        every bench.py workload line (tools/bench_all.sh); lines:<a,b,..> a subset
 #   line:<key>   one workload line: key as in prof:<key>
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512 xdphbm frames
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
+#   pcie / hostpack / hoststream   the host-fed feed's microbenchmarks and infw_classify_host (tools/micro, tools/host_stream.py)
 #   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: keyorder split fstride)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
 set -u
@@ -29,6 +30,7 @@ args_of() {  # bench.py arguments of a workload key
     cfg2dw) echo "--templates 1000000 --key-order workload" ;;
     cfg2w)  echo "--key-order workload" ;;
     xdphbm) echo "--xdp-ring hbm" ;;
+    xdphp)  echo "--xdp-ring host-packed --steps 10 --warmup 2" ;;
     fused80)  echo "--from-frames 80 --fused" ;;
     fused256) echo "--from-frames 256 --fused" ;;
     fused512) echo "--from-frames 512 --fused" ;;
@@ -49,10 +51,15 @@ step() {
       [ $rc -eq 0 ] || return $rc
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || rc=$?
       tail -1 $O/smoke.log ;;
-    test:*)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" \
-          > $O/pytest_${s#test:}.log 2>&1 || rc=$?
-      tail -3 $O/pytest_${s#test:}.log ;;
+    test:*)  # test:a,b,c -> pytest -k "a or b or c" (no spaces: the step list is word-split on the way in)
+      local k=${s#test:} lg=$O/pytest_$(echo ${s#test:} | tr , _).log
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+          -k "$(echo $k | sed 's/,/ or /g')" > $lg 2>&1 || rc=$?
+      tail -3 $lg ;;
+    sweep|sweep:*)  # infw_classify_xdp_host over packer threads x chunk (tools/xdp_host_sweep.py); sweep:<args joined by +>
+      local sa=""; [ "$s" != sweep ] && sa=$(echo ${s#sweep:} | tr + ' ')
+      timeout -k 10 600 python -u tools/xdp_host_sweep.py --trace $sa >> $O/xdp_host_sweep.jsonl 2>> $O/xdp_host_sweep.trace || rc=$?
+      tail -30 $O/xdp_host_sweep.jsonl ;;
     bench)
       timeout -k 10 300 python -u bench.py > $O/bench_default.log 2>&1 || rc=$?
       tail -1 $O/bench_default.log | cut -c1-400 ;;
@@ -70,6 +77,23 @@ step() {
       bash tools/profile.sh ${TAG}_${s#prof:} $a --steps 5 --warmup 1 --no-cpu-baseline || rc=$? ;;
     micro)
       timeout -k 10 300 ./tools/micro/gather > $O/gather.jsonl 2>&1 || rc=$? ;;
+    pcie)     # GPU reads of pinned host memory and the SDMA 2D header gather (tools/micro/pcie.hip, built beforehand)
+      timeout -k 10 300 ./tools/micro/pcie > $O/pcie.jsonl 2>&1 || rc=$?
+      tail -4 $O/pcie.jsonl ;;
+    hostpack) # the host packer alone on the box's cores (CPU only; tools/micro/hostpack.cpp, built beforehand)
+      (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | grep -E "Model name|^CPU\(s\)|NUMA node\(s\)") > $O/host_cpu.txt 2>&1
+      timeout -k 10 300 ./tools/micro/hostpack --umem-gib 8 --descs 16 --threads 1,4,8,16 > $O/hostpack.jsonl 2>&1 || rc=$?
+      tail -4 $O/hostpack.jsonl ;;
+    hostpackx) # the packer's per-core rate by input order and output memory (32 GiB umem, 2048-B chunks)
+      for cfg in "--keep 1 --out vector" "--keep 4 --out vector" "--keep 4 --out pinned" "--keep 4 --out registered" \
+                 "--keep 1 --shuffle --out pinned"; do
+        timeout -k 10 300 ./tools/micro/hostpack --umem-gib 32 --descs 16 --thp 1 --threads 1,16 $cfg \
+            >> $O/hostpackx.jsonl 2>&1 || { rc=$?; break; }
+      done
+      tail -12 $O/hostpackx.jsonl ;;
+    hoststream) # infw_classify_host: SoA tuples in host memory, chunked H2D / classify / D2H
+      timeout -k 10 300 python -u tools/host_stream.py > $O/host_stream.json 2>&1 || rc=$?
+      tail -3 $O/host_stream.json ;;
     ab:*)
       timeout -k 10 1000 bash tools/ab.sh $TAG ${s#ab:} > $O/ab_${s#ab:}.log 2>&1 || rc=$?
       tail -5 $O/ab_${s#ab:}.log ;;
