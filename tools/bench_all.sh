@@ -16,6 +16,7 @@ run() {  # name, args...
 run cfg2 --steps 30
 run cfg2_compact --layout compact --no-cpu-baseline --steps 30
 run cfg1 --cfg 1 --batch 67108864 --no-cpu-baseline --steps 30
+run cfg1_compact --cfg 1 --batch 67108864 --layout compact --no-cpu-baseline --steps 30
 run cfg4 --cfg 4 --no-cpu-baseline --steps 30
 run cfg4_1m --cfg 4 --prefixes 1000000 --no-cpu-baseline --steps 30
 run cfg2_uniform --uniform --no-cpu-baseline --steps 30
@@ -26,6 +27,9 @@ run cfg2_frames_fused --from-frames 128 --fused --no-cpu-baseline --steps 20
 run cfg2_xdp_hbm --xdp-ring hbm --no-cpu-baseline --steps 20
 run cfg2_xdp_host --xdp-ring host --no-cpu-baseline --steps 10 --warmup 2
 run cfg2_xdp_registered --xdp-ring registered --no-cpu-baseline --steps 10 --warmup 2
+# the host-fed path: umem and rings in pageable memory, packed by the library's host threads (infw_classify_xdp_host)
+run cfg2_xdp_host_packed --xdp-ring host-packed --no-cpu-baseline --steps 10 --warmup 2
+run cfg2_xdp_host_packed_interleaved --xdp-ring host-packed --umem-order packet --no-cpu-baseline --steps 10 --warmup 2
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
 # the library's one-process shape: one context over N device slots (all on this GPU), a thread + stream per slot
 run inproc_n1 --in-process --gpus 1 --slots-on-gpu0 --global-packets 1073741824 --steps 5 --warmup 1 --no-line-rates

@@ -9,6 +9,7 @@
 #   line:<key>   one workload line: key as in prof:<key>
 #   prof:<key>   rocprofv3 kernel trace + PMC passes of one workload (tools/profile.sh) into gpurun_out/prof_<tag>_<key>;
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512 xdphbm frames
+#   lat:<key>    latency-attribution PMC passes of one workload (tools/profile_lat.sh)
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
 #   pcie / hostpack / hoststream   the host-fed feed's microbenchmarks and infw_classify_host (tools/micro, tools/host_stream.py)
 #   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: keyorder split fstride)
@@ -23,6 +24,7 @@ args_of() {  # bench.py arguments of a workload key
     cfg2)   echo "" ;;
     cfg2c)  echo "--layout compact" ;;
     cfg1)   echo "--cfg 1 --batch 67108864" ;;
+    cfg1c)  echo "--cfg 1 --batch 67108864 --layout compact" ;;
     cfg4)   echo "--cfg 4" ;;
     cfg4m)  echo "--cfg 4 --prefixes 1000000" ;;
     cfg2u)  echo "--uniform" ;;
@@ -75,6 +77,9 @@ step() {
       local a; a=$(args_of ${s#prof:}) || return 2
       [ "${s#prof:}" = cfg3 ] && a="--global-packets 1073741824"
       bash tools/profile.sh ${TAG}_${s#prof:} $a --steps 5 --warmup 1 --no-cpu-baseline || rc=$? ;;
+    lat:*)       # latency attribution PMC passes of one workload (tools/profile_lat.sh) into gpurun_out/lat_<tag>_<key>
+      local a; a=$(args_of ${s#lat:}) || return 2
+      bash tools/profile_lat.sh ${TAG}_${s#lat:} $a || rc=$? ;;
     micro)
       timeout -k 10 300 ./tools/micro/gather > $O/gather.jsonl 2>&1 || rc=$? ;;
     pcie)     # GPU reads of pinned host memory and the SDMA 2D header gather (tools/micro/pcie.hip, built beforehand)
