@@ -118,7 +118,10 @@ $(TSAN_DIR)/libinfw.so: $(TSAN_OBJS) $(HIP_OBJS)
 	g++ -shared -fsanitize=thread -o $@ $^ -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 $(TSAN_DIR)/tsan_abi: tools/tsan_abi.cpp $(TSAN_DIR)/libinfw.so
 	g++ $(TSAN_FLAGS) -o $@ tools/tsan_abi.cpp -L$(TSAN_DIR) -linfw -Wl,-rpath,'$$ORIGIN'
-tsan-host: $(TSAN_DIR)/tsan_abi
+# the packer pool of infw_classify_xdp_host alone (no device), its coordinator played by the test
+$(TSAN_DIR)/tsan_hostpool: tools/tsan_hostpool.cpp $(TSAN_DIR)/hostfeed.cpp.o
+	g++ $(TSAN_FLAGS) -pthread -o $@ tools/tsan_hostpool.cpp $(TSAN_DIR)/hostfeed.cpp.o
+tsan-host: $(TSAN_DIR)/tsan_abi $(TSAN_DIR)/tsan_hostpool
 
 clean:
 	rm -rf $(OBJ) $(OUT) oracle/build

@@ -4,7 +4,9 @@
  * XDP_UMEM_REG), page-locked for the GPU with infw_host_register; the RX ring's descriptors name frames in it;
  * infw_classify_xdp reads the frames and the descriptors in place over PCIe and writes the result words and verdicts
  * into the daemon's (registered) host arrays.  One ring per interface queue: the frames of ifindex 7 and of ifindex
- * 8 are two calls.
+ * 8 are two calls.  Then the same frames through the host-fed path, infw_classify_xdp_host, with the memory as the
+ * daemon allocated it (pageable, unregistered — the form a socket's mmapped ring has): both rings in one call.  Before
+ * any registration, infw_classify_xdp must refuse that memory with -EFAULT rather than let the GPU fault on it.
  *
  *   the XDP entry per frame (kernel.c:459-462, ethertype / L4 extraction :95-174, :412-440)
  *   statsMap.Lookup (statistics.go:127):  infw_stats_read
@@ -96,15 +98,42 @@ int main(int argc, char **argv) {
         rx[i].len = pk[i].len;
         rx[i].options = 0;
     }
+    /* the two interface rings as infw_classify_xdp_host takes them (one call) */
+    const struct infw_xdp_ring rings[2] = {{umem, rx, N - 1, 7, 0, results, verdicts},
+                                           {umem, rx + N - 1, 1, 8, 0, results + N - 1, verdicts + N - 1}};
     if (host_only) {
-        const int rc = infw_classify_xdp(ctx, 0, umem, rx, N - 1, 7, results, verdicts, NULL);
+        int rc = infw_classify_xdp(ctx, 0, umem, rx, N - 1, 7, results, verdicts, NULL);
         if (rc != -ENODEV) {
             fprintf(stderr, "host-only classify_xdp returned %d, want -ENODEV\n", rc);
             return 1;
         }
+        rc = infw_classify_xdp_host(ctx, 0, rings, 2, 0);
+        if (rc != -ENODEV) {
+            fprintf(stderr, "host-only classify_xdp_host returned %d, want -ENODEV\n", rc);
+            return 1;
+        }
+        /* the host packer alone needs no device: frame 0's tuple as kernel.c reads it */
+        uint32_t s4[N], ifx[N], plen[N], meta[N], l4[N];
+        uint8_t tail[768];
+        const struct infw_batch_soa_c_out o = {s4, tail, ifx, plen, meta, l4};
+        CHECK(infw_pack_xdp_host(umem, rx, N, 7, &o));
+        if (s4[0] != (10u | 1u << 8 | 2u << 16 | 3u << 24) || ifx[0] != 7 || plen[0] != 100 ||
+            meta[0] != (0x0800u | 6u << 16 | 100u << 24) || l4[0] != (40000u >> 8 | (40000u & 0xFF) << 8 | 80u << 24)) {
+            fprintf(stderr, "pack_xdp_host: frame 0 packed as %08x %u %u %08x %08x\n", s4[0], ifx[0], plen[0], meta[0],
+                    l4[0]);
+            return 1;
+        }
         infw_destroy(ctx);
-        printf("xdp_demo OK (host): classify_xdp refused without a device, ABI %d\n", infw_abi_version());
+        printf("xdp_demo OK (host): classify_xdp and classify_xdp_host refused without a device, the host packer "
+               "alone packed %d frames, ABI %d\n", N, infw_abi_version());
         return 0;
+    }
+    {
+        const int rc = infw_classify_xdp(ctx, 0, umem, rx, N - 1, 7, results, verdicts, NULL);
+        if (rc != -EFAULT) {
+            fprintf(stderr, "classify_xdp on pageable memory returned %d, want -EFAULT\n", rc);
+            return 1;
+        }
     }
     CHECK(infw_host_register(ctx, umem, CHUNKS * CHUNK));
     CHECK(infw_host_register(ctx, rx, 4096));
@@ -150,9 +179,34 @@ int main(int argc, char **argv) {
     CHECK(infw_host_unregister(ctx, rx));
     CHECK(infw_host_unregister(ctx, results));
     CHECK(infw_host_unregister(ctx, verdicts));
+
+    /* the host-fed path over the same memory, now ordinary pageable memory again: the library's packer threads read
+     * the frames on the CPU; both rings in one synchronous call; same verdicts, counters doubled */
+    memset(results, 0xFF, 4 * N);
+    memset(verdicts, 7, N);
+    CHECK(infw_classify_xdp_host(ctx, 0, rings, 2, 0));
+    for (int i = 0; i < N; i++)
+        if (verdicts[i] != want_v[i] || results[i] != want_r[i]) {
+            fprintf(stderr, "host-fed frame %d: verdict %u result 0x%x, want %u 0x%x\n", i, verdicts[i], results[i],
+                    want_v[i], want_r[i]);
+            return 1;
+        }
+    struct ruleStatistics_st all[INFW_MAX_TARGETS];
+    CHECK(infw_stats_read_all(ctx, all));
+    uint64_t allow2 = 0, deny2 = 0, allow2_b = 0, deny2_b = 0;
+    for (int rule = 1; rule < 100; rule++) {
+        allow2 += all[rule].allow_stats.packets, allow2_b += all[rule].allow_stats.bytes;
+        deny2 += all[rule].deny_stats.packets, deny2_b += all[rule].deny_stats.bytes;
+    }
+    if (allow2 != 2 * allow || allow2_b != 2 * allow_b || deny2 != 2 * deny || deny2_b != 2 * deny_b) {
+        fprintf(stderr, "host-fed counters: allow %llu/%llu deny %llu/%llu\n", (unsigned long long)allow2,
+                (unsigned long long)allow2_b, (unsigned long long)deny2, (unsigned long long)deny2_b);
+        return 1;
+    }
     infw_destroy(ctx);
     free(umem), free(rx), free(results), free(verdicts);
-    printf("xdp_demo OK: %d frames in 2 rings, allow %llu (%llu B), deny %llu (%llu B), ABI %d\n", N,
+    printf("xdp_demo OK: %d frames in 2 rings, allow %llu (%llu B), deny %llu (%llu B); pageable memory refused by the "
+           "device read (-EFAULT) and classified by the host-fed path, ABI %d\n", N,
            (unsigned long long)allow, (unsigned long long)allow_b, (unsigned long long)deny,
            (unsigned long long)deny_b, infw_abi_version());
     return 0;

@@ -53,11 +53,12 @@ def test_c_xdp_caller_host_only(tmp_path):
 
 @pytest.mark.gpu
 def test_c_xdp_caller_on_device(tmp_path):
-    """A daemon's own (registered) umem, ring and result arrays through infw_classify_xdp, two interface rings."""
+    """A daemon's own (registered) umem, ring and result arrays through infw_classify_xdp, two interface rings; the
+    same memory unregistered refused by it (-EFAULT) and classified by the host-fed path (infw_classify_xdp_host)."""
     exe = build_xdp_demo(tmp_path)
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    assert "allow 2 (600 B), deny 1 (100 B)" in out.stdout
+    assert "allow 2 (600 B), deny 1 (100 B); pageable memory refused" in out.stdout
 
 
 def test_c_caller_host_only(tmp_path):
