@@ -66,7 +66,8 @@ def main():
             bl = s.get("bench_line_under_kernel_trace", {})
             assert bl.get("build_id") in (None, d.get("build_id")), (name, bl.get("build_id"), d.get("build_id"))
             stream = (r.get("line_rates") or {}).get("stream_GB_per_s")
-            row.update(rocprof_ms=s["avg_ns_per_classification"] / 1e6, hbm_B=s["hbm_bytes_per_packet"],
+            rings = (r.get("xdp_ring") or {}).get("rings") or 1  # AF_XDP: one launch per ring, the line's time per step
+            row.update(rocprof_ms=s["avg_ns_per_classification"] * rings / 1e6, hbm_B=s["hbm_bytes_per_packet"],
                        hits=s["l2_hits_per_packet"], misses=s["l2_misses_per_packet"],
                        fabric_req=s["ea_rdreq_per_packet"], profile=f"profiles/{tag}_{key}")
             if stream and k_ms:  # per step: the step's packets over the step's kernel time (AF_XDP: one launch per ring)

@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--no-thp", action="store_true")
     ap.add_argument("--order", choices=("ring", "packet"), default="ring",
                     help="umem layout (bench.py --umem-order)")
+    ap.add_argument("--per-call", default="",
+                    help="comma-separated descriptors per call (summed over the rings: each call takes an equal "
+                         "slice of every ring, as a daemon polling its sockets would): the per-call overhead sweep "
+                         "at the default thread count and chunk, after the threads x chunk sweep")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -68,7 +72,8 @@ def main():
     setup_s = time.perf_counter() - t0
     print(json.dumps({"frames": n, "stride": STRIDE, "rings": len(rings), "setup_s": round(setup_s, 1),
                       "thp": not args.no_thp, "order": args.order, "cpus": os.cpu_count(),
-                      "affinity": len(os.sched_getaffinity(0))}), flush=True)
+                      "affinity": len(os.sched_getaffinity(0)),
+                      "loadavg_1m": os.getloadavg()[0]}), flush=True)
     if args.trace:
         clf.set_option("trace", 8)
     ref = None
@@ -87,8 +92,31 @@ def main():
             same = bool(np.array_equal(words, ref))
             print(json.dumps({"chunk": chunk, "threads": t, "ms": round(best * 1e3, 3),
                               "Mpps": round(n / best / 1e6, 1), "Mpps_per_thread": round(n / best / 1e6 / t, 1),
-                              "h2d_GBps": round(n * 28 / best / 1e9, 2), "same_words": same}), flush=True)
+                              "h2d_GBps": round(n * 28 / best / 1e9, 2), "same_words": same,
+                              "loadavg_1m": os.getloadavg()[0]}), flush=True)
             assert same
+    for per in [int(x) for x in args.per_call.split(",") if x]:
+        clf.set_option("host_threads", 0)
+        q = max(1, per // len(rings))  # descriptors per ring per call
+
+        def calls():
+            for a in range(0, max(r[2] for r in rings), q):
+                yield [(r[0], r[1][a:a + q], min(q, r[2] - a), r[3], r[4][a:a + q], None) for r in rings if a < r[2]]
+        batches = list(calls())
+        for b in batches[:4]:
+            clf.classify_xdp_host(b)  # warm
+        best = 1e30
+        for _ in range(args.reps):
+            s0 = time.perf_counter()
+            for b in batches:
+                clf.classify_xdp_host(b)
+            best = min(best, time.perf_counter() - s0)
+        words = np.concatenate([r[4].numpy() for r in rings])
+        assert np.array_equal(words, ref)
+        print(json.dumps({"per_call": per, "calls": len(batches), "ms": round(best * 1e3, 3),
+                          "us_per_call": round(best / len(batches) * 1e6, 1), "Mpps": round(n / best / 1e6, 1),
+                          "threads": clf.option("host_threads") or "auto", "same_words": True,
+                          "loadavg_1m": os.getloadavg()[0]}), flush=True)
 
 
 if __name__ == "__main__":
