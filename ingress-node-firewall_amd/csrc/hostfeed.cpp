@@ -45,9 +45,10 @@ HostPackPool::~HostPackPool() {
     for (auto &w : workers_) w.join();
 }
 
-void HostPackPool::begin(const std::vector<XdpChunk> *chunks, std::vector<infw_hostpack_out> slots, uint64_t released) {
+void HostPackPool::begin(const std::vector<XdpChunk> *chunks, const std::vector<XdpSeg> *segs, uint64_t released) {
+    // closed_ is set: no worker reads the fields below while they are written
     chunks_ = chunks;
-    slots_ = std::move(slots);
+    segs_ = segs;
     const size_t K = chunks->size();
     unit_base_.assign(K + 1, 0);
     for (size_t k = 0; k < K; k++)
@@ -59,7 +60,8 @@ void HostPackPool::begin(const std::vector<XdpChunk> *chunks, std::vector<infw_h
     pack_ns_.store(0);
     release_wait_ns_.store(0);
     released_.set(base_ + released);
-    job_.set(++gen_);  // publishes the job (the signal's mutex orders the fields above before the workers' reads)
+    closed_.store(false, std::memory_order_seq_cst);  // publishes the job to workers that check it
+    if (unit_base_.back() > 2) job_.set(++gen_);        // a call of one or two units wakes no worker
 }
 
 void HostPackPool::end(bool abort) {
@@ -67,9 +69,20 @@ void HostPackPool::end(bool abort) {
         abort_.store(true);
         released_.set(base_ + chunks_->size());
     }
-    idle_.wait_at_least(gen_ * n_threads_);
+    closed_.store(true, std::memory_order_seq_cst);
+    // a worker inside the job finishes at most the unit it holds; one that arrives now sees closed_ and leaves
+    for (int i = 0; active_.load(std::memory_order_seq_cst) != 0; i++) {
+        if (i < 4096) {
+#if defined(__x86_64__)
+            _mm_pause();
+#endif
+        } else {
+            std::this_thread::yield();
+        }
+    }
     base_ += chunks_->size();
     chunks_ = nullptr;
+    segs_ = nullptr;
 }
 
 void HostPackPool::advance_frontier() {
@@ -81,39 +94,86 @@ void HostPackPool::advance_frontier() {
     if (frontier_ != f0) packed_.set(base_ + frontier_);
 }
 
+void HostPackPool::pack_unit(uint64_t u, uint64_t k) {
+    const XdpChunk &c = (*chunks_)[k];
+    const uint64_t a = std::min(c.n, (u - unit_base_[k]) * kPackUnit), b = std::min(c.n, a + kPackUnit);
+    if (a < b && !abort_.load(std::memory_order_relaxed)) pack_chunk_range(c, *segs_, a, b);
+}
+
+bool HostPackPool::claim_and_pack(bool coordinator) {
+    using clk = std::chrono::steady_clock;
+    const uint64_t U = unit_base_.back();
+    uint64_t u, k;
+    auto chunk_of = [&](uint64_t unit) {
+        return (uint64_t)(std::upper_bound(unit_base_.begin(), unit_base_.end(), unit) - unit_base_.begin()) - 1;
+    };
+    auto t0 = clk::now();
+    if (coordinator) {  // only units of released chunks: the coordinator is the one that releases
+        u = next_unit_.load(std::memory_order_relaxed);
+        for (;;) {
+            if (u >= U) return false;
+            k = chunk_of(u);
+            if (base_ + k + 1 > released_.get()) return false;
+            if (next_unit_.compare_exchange_weak(u, u + 1, std::memory_order_relaxed)) break;
+        }
+    } else {
+        u = next_unit_.fetch_add(1, std::memory_order_relaxed);
+        if (u >= U) return false;
+        k = chunk_of(u);
+        released_.wait_at_least(base_ + k + 1);
+    }
+    const auto t1 = clk::now();
+    pack_unit(u, k);
+    const auto t2 = clk::now();
+    release_wait_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
+                               std::memory_order_relaxed);
+    pack_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count(), std::memory_order_relaxed);
+    if (done_[k].fetch_add(1, std::memory_order_acq_rel) + 1 == unit_base_[k + 1] - unit_base_[k]) advance_frontier();
+    return true;
+}
+
+void HostPackPool::help_until_packed(uint64_t k) {
+    const uint64_t target = base_ + k + 1;
+    while (packed_.get() < target)
+        if (!claim_and_pack(true)) {
+            packed_.wait_at_least(target);  // the last units are on workers
+            return;
+        }
+}
+
 void HostPackPool::work() {
     uint64_t seen = 0;
     for (;;) {
         job_.wait_at_least(seen + 1);
         seen = job_.get();
         if (quit_.load()) return;
-        const std::vector<XdpChunk> &ch = *chunks_;
-        const uint64_t NS = slots_.size(), base = base_, U = unit_base_.back();
-        using clk = std::chrono::steady_clock;
-        uint64_t wait_ns = 0, busy_ns = 0, k = 0;
-        for (;;) {
-            const uint64_t u = next_unit_.fetch_add(1, std::memory_order_relaxed);
-            if (u >= U) break;
-            while (unit_base_[k + 1] <= u) k++;  // a worker's units only grow, so its chunk index does too
-            const auto t0 = clk::now();
-            released_.wait_at_least(base + k + 1);
-            const auto t1 = clk::now();
-            wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-            const XdpChunk &c = ch[k];
-            const uint64_t a = std::min(c.n, (u - unit_base_[k]) * kPackUnit), b = std::min(c.n, a + kPackUnit);
-            if (a < b && !abort_.load(std::memory_order_relaxed)) {
-                const infw_hostpack_out &s = slots_[k % NS];
-                const infw_hostpack_out o{s.saddr4 + a, s.v6tail + a / INFW_V6_GROUP * (12ull * INFW_V6_GROUP),
-                                          nullptr, s.pkt_len + a, s.meta + a, s.l4word + a};
-                infw_hostpack_xdp<16, false>(c.umem, c.descs + a, b - a, c.ifindex, o);
+        active_.fetch_add(1, std::memory_order_seq_cst);
+        if (!closed_.load(std::memory_order_seq_cst))
+            while (claim_and_pack(false)) {
             }
-            busy_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t1).count();
-            if (done_[k].fetch_add(1, std::memory_order_acq_rel) + 1 == unit_base_[k + 1] - unit_base_[k])
-                advance_frontier();
+        active_.fetch_sub(1, std::memory_order_seq_cst);
+    }
+}
+
+void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64_t a, uint64_t b) {
+    constexpr uint64_t G = INFW_V6_GROUP;
+    for (uint32_t si = c.seg0; si < c.seg1; si++) {
+        const XdpSeg &s = segs[si];
+        const uint64_t s0 = std::max(a, s.pos), s1 = std::min(b, s.pos + s.n);
+        for (uint64_t p = s0; p < s1;) {
+            const uint64_t g0 = p & ~(G - 1);
+            uint32_t rank = 0;  // IPv6 packets an earlier segment put into this group: they hold its first tail slots
+            uint64_t e = s1;
+            if (p != g0) {  // (the same thread packed them: units start on group boundaries)
+                for (uint64_t q = g0; q < p; q++) rank += (c.out.meta[q] & 0xFFFFu) == 0x86DDu;
+                e = std::min(s1, g0 + G);  // up to the group's end, so the packer's group boundaries stay aligned
+            }
+            const infw_hostpack_out o{c.out.saddr4 + p, c.out.v6tail + g0 / G * (12 * G) + 12 * rank,
+                                      c.mixed ? c.out.ifindex + p : nullptr, c.out.pkt_len + p, c.out.meta + p,
+                                      c.out.l4word + p};
+            infw_hostpack_xdp<16, false>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex, o);
+            p = e;
         }
-        pack_ns_.fetch_add(busy_ns);
-        release_wait_ns_.fetch_add(wait_ns);
-        idle_.set(idle_total_.fetch_add(1) + 1);
     }
 }
 
