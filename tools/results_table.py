@@ -7,7 +7,9 @@ run's launches); roofline.frac (algorithmic bytes / HIP-event time / 8 TB/s); HB
 requests (TCC_EA0_RDREQ) x 128 B per second against the stream bandwidth the same line measured in its own process,
 and its inverse (the most the kernel could gain at today's lines per packet if every random line moved at the
 streaming rate).  Lines whose build id differs from the profile's are refused.
-Usage: tools/results_table.py <pass> (e.g. r06z)  -> markdown on stdout, JSON in profiles/<pass>/results.json"""
+Usage: tools/results_table.py <pass> [<override pass>]  (e.g. r06z r06w: lines present in profiles/<override>/lines
+replace the pass's own — a component re-measured after a host-side change at the same kernel build)
+  -> markdown on stdout, JSON in profiles/<pass>/results.json"""
 import json
 import os
 import sys
@@ -43,9 +45,12 @@ def last_json(path):
 
 def main():
     tag = sys.argv[1]
+    over = sys.argv[2] if len(sys.argv) > 2 else None
     rows, out = [], {}
     for name in ORDER:
         p = os.path.join(ROOT, "profiles", tag, "lines", f"{name}.log")
+        if over and os.path.exists(os.path.join(ROOT, "profiles", over, "lines", f"{name}.log")):
+            p = os.path.join(ROOT, "profiles", over, "lines", f"{name}.log")
         if not os.path.exists(p):
             continue
         d = last_json(p)
@@ -55,7 +60,7 @@ def main():
         # in-process lines: N slots sharing the device, each slot's kernel time overlapping the others' (their
         # wall time per step stands for the launch)
         k_ms = r.get("kernel_ms_avg") or (d["ms_per_step"] if per_slot else None)
-        row = {"line": name, "build_id": d.get("build_id"), "Gpps": d["value"] / 1e3,
+        row = {"line": name, "source": os.path.relpath(p, ROOT), "build_id": d.get("build_id"), "Gpps": d["value"] / 1e3,
                "kernel": r.get("kernel") or d.get("kernel"),
                "packets_per_launch": n, "kernel_ms_hip": k_ms, "frac": r.get("frac"), "bound": r.get("bound"),
                "algo_B": r.get("algorithmic_bytes_per_packet")}
@@ -79,16 +84,16 @@ def main():
 
     def f(v, fmt):
         return format(v, fmt) if isinstance(v, (int, float)) else "—"
-    print("| workload | kernel (registry name) | packets/launch | Gpps | kernel ms (HIP events) | kernel ms (rocprof) "
+    print("| workload | kernel (registry name) | Gpps | kernel ms (HIP events) | kernel ms (rocprof) "
           "| frac | HBM B/pkt (PMC) vs algorithmic | L2 hits / misses per packet | line traffic (of stream) | headroom |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
         gpps = f(r["Gpps"], ".3f") if r["Gpps"] < 2 else f(r["Gpps"], ".1f")
         hb = f"{r['hbm_B']:.1f} vs {r['algo_B']:.1f} ({r['hbm_B'] / r['algo_B']:.2f}×)" if "hbm_B" in r else "—"
         hm = f"{r['hits']:.2f} / {r['misses']:.2f}" if "hits" in r else "—"
         lt = f"{r['line_TBps']:.1f} TB/s ({r['line_frac']:.2f})" if "line_TBps" in r else "—"
         frac = f(r["frac"], ".3f") + (" (PCIe)" if r.get("bound") == "pcie" else "")
-        print(f"| {LABEL[r['line']]} | `{r['kernel']}` | {r['packets_per_launch']:,} | {gpps} | {f(r['kernel_ms_hip'], '.3f')} "
+        print(f"| {LABEL[r['line']]} | `{r['kernel']}` | {gpps} | {f(r['kernel_ms_hip'], '.3f')} "
               f"| {f(r.get('rocprof_ms'), '.3f')} | {frac} | {hb} | {hm} | {lt} | {f(r.get('headroom'), '.2f')} |")
 
 
