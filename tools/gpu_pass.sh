@@ -12,7 +12,6 @@
 #   lat:<key>    latency-attribution PMC passes of one workload (tools/profile_lat.sh)
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
 #   pcie / hostpack / hoststream   the host-fed feed's microbenchmarks and infw_classify_host (tools/micro, tools/host_stream.py)
-#   ab:<exp>     a same-box A/B of bench lines (tools/ab.sh <tag> <exp>: keyorder split fstride)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
 set -u
 TAG=${1:?tag}; shift
@@ -99,9 +98,6 @@ step() {
     hoststream) # infw_classify_host: SoA tuples in host memory, chunked H2D / classify / D2H
       timeout -k 10 300 python -u tools/host_stream.py > $O/host_stream.json 2>&1 || rc=$?
       tail -3 $O/host_stream.json ;;
-    ab:*)
-      timeout -k 10 1000 bash tools/ab.sh $TAG ${s#ab:} > $O/ab_${s#ab:}.log 2>&1 || rc=$?
-      tail -5 $O/ab_${s#ab:}.log ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
   echo "step $s rc=$rc"
