@@ -685,13 +685,26 @@ def run_rank(args):
                           "frames": infw.INPUT_FRAMES}[args.layout])
     host_feed = None
     if args.xdp_ring == "host-packed":
-        # per step over PCIe: each pipeline chunk of C descriptors carries the family-compact streams without ifindex
-        # (saddr4, pkt_len, meta, l4word: 16 B/packet) and its groups' whole 768-B v6tail blocks; result words back
+        # per step over PCIe, as infw_classify_xdp_host cuts the rings: chunks of at most C descriptors running on
+        # from one ring into the next (chunk 0: 512K, or a quarter of a call under four of those, >= 32K); a chunk of
+        # n descriptors is one H2D copy of 28 B x S (S = n rounded up to 64: saddr4, pkt_len, meta, l4word and the
+        # groups' whole 768-B v6tail blocks), 32 B x S when its rings carry several ifindexes; result words back
         C = ((args.xdp_chunk or (1 << 19)) + 511) // 512 * 512
-        h2d = 0
-        for _, nr, _ in rings:
-            full, rem = divmod(nr, C)
-            h2d += full * 28 * C + ((12 * C + 4 * rem + -(-rem // 64) * 768) if rem else 0)
+        total = sum(nr for _, nr, _ in rings)
+        if not args.xdp_chunk and total < 4 * C:
+            C = min(C, max(32768, ((total + 3) // 4 + 4095) // 4096 * 4096))
+        h2d, fill, ifs = 0, 0, set()
+        for ifv, nr, _ in rings:
+            a = 0
+            while a < nr:
+                take = min(C - fill, nr - a)
+                ifs.add(ifv)
+                fill, a = fill + take, a + take
+                if fill == C:
+                    h2d += (32 if len(ifs) > 1 else 28) * C
+                    fill, ifs = 0, set()
+        if fill:
+            h2d += (32 if len(ifs) > 1 else 28) * (-(-fill // 64) * 64)
         step_s = sum(kern_ms) / len(kern_ms) / 1e3
         threads = clf.option("host_threads") or min(usable_cores(), 16)
         host_feed = {"host_threads": threads, "usable_cores": usable_cores(), "chunk": C,
@@ -699,7 +712,8 @@ def run_rank(args):
                      "pcie_d2h_GBps": round(4 * n / step_s / 1e9, 2),
                      "pcie_h2d_bytes_per_packet": round(h2d / max(n, 1), 2),
                      "pcie_h2d_peak_GBps": PCIE_H2D_GBS, "pcie_h2d_frac": round(h2d / step_s / 1e9 / PCIE_H2D_GBS, 3),
-                     "Mpps_per_host_thread": round(n / step_s / 1e6 / threads, 1)}
+                     # the calling thread packs too (it packs whenever it would otherwise wait for the packers)
+                     "Mpps_per_host_thread": round(n / step_s / 1e6 / (threads + 1), 1)}
     if args.xdp_ring:
         extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "umem_order": args.umem_order, "chunk": stride,
                                    "rings": len(rings),
