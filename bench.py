@@ -713,7 +713,11 @@ def run_rank(args):
                      "pcie_h2d_bytes_per_packet": round(h2d / max(n, 1), 2),
                      "pcie_h2d_peak_GBps": PCIE_H2D_GBS, "pcie_h2d_frac": round(h2d / step_s / 1e9 / PCIE_H2D_GBS, 3),
                      # the calling thread packs too (it packs whenever it would otherwise wait for the packers)
-                     "Mpps_per_host_thread": round(n / step_s / 1e6 / (threads + 1), 1)}
+                     "Mpps_per_host_thread": round(n / step_s / 1e6 / (threads + 1), 1),
+                     # the packers share the host with whatever else runs on it: the spread of the timed steps and the
+                     # host's load average say how much of the step the CPUs were really ours
+                     "step_ms_min": round(min(kern_ms), 3), "step_ms_median": round(float(np.median(kern_ms)), 3),
+                     "step_ms_max": round(max(kern_ms), 3), "host_loadavg_1m": round(os.getloadavg()[0], 1)}
     if args.xdp_ring:
         extra_pipe = {"xdp_ring": {"umem": args.xdp_ring, "umem_order": args.umem_order, "chunk": stride,
                                    "rings": len(rings),
