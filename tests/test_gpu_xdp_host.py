@@ -206,3 +206,20 @@ def test_xdp_host_small_calls_back_to_back(setup):
         assert bad.size == 0, (bad[:5], g[bad[:5]], w[bad[:5]])
     print(f"[xdp_host small calls] {len(lat)} calls of up to 3 x 300 descriptors: median "
           f"{np.median(lat) * 1e6:.0f} us, p90 {np.percentile(lat, 90) * 1e6:.0f} us per call")
+
+
+def test_xdp_host_optional_outputs(setup):
+    """Rings that want only verdicts, only result words, or neither (statistics only) in one call, sharing chunks:
+    each ring gets exactly what it asked for and the counters still cover every ring."""
+    wl, clf, m = setup
+    rings = rings_of(wl, 31000, [700, 900, 1100], "aligned", seed=23)
+    want, wver, wst = oracle_of(m, rings)
+    res = np.full(900, 0xFFFFFFFF, np.uint32)
+    ver = np.full(700, 7, np.uint8)
+    args = [(rings[0]["umem"], rings[0]["desc"], 700, rings[0]["ifindex"], None, ver),
+            (rings[1]["umem"], rings[1]["desc"], 900, rings[1]["ifindex"], res, None),
+            (rings[2]["umem"], rings[2]["desc"], 1100, rings[2]["ifindex"], None, None)]
+    clf.stats_reset()
+    clf.classify_xdp_host(args, chunk=512)  # chunks of 512: every chunk boundary inside or between rings
+    assert np.array_equal(ver, wver[0]) and np.array_equal(res, want[1])
+    assert np.array_equal(clf.stats_read_all(), wst)
