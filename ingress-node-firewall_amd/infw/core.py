@@ -472,6 +472,14 @@ class HostSoa:
     def arrays(self):
         return (self.saddr, self.ifindex, self.pkt_len, self.meta, self.l4word)
 
+    def slice(self, a: int, b: int) -> "HostSoa":
+        """Packets [a, b) as views of the same memory (no copy)."""
+        h = HostSoa.__new__(HostSoa)
+        h.n = b - a
+        h.saddr, h.ifindex, h.pkt_len = self.saddr[a:b], self.ifindex[a:b], self.pkt_len[a:b]
+        h.meta, h.l4word = self.meta[a:b], self.l4word[a:b]
+        return h
+
 
 def pack_xdp_host(umem: np.ndarray, descs: np.ndarray, ifindex: int) -> Dict[str, np.ndarray]:
     """infw_pack_xdp_host: the host packer of infw_classify_xdp_host on the calling thread — one AF_XDP ring's frames

@@ -96,8 +96,9 @@ step() {
       done
       tail -12 $O/hostpackx.jsonl ;;
     hoststream) # infw_classify_host: SoA tuples in host memory, chunked H2D / classify / D2H
-      timeout -k 10 300 python -u tools/host_stream.py > $O/host_stream.json 2>&1 || rc=$?
-      tail -3 $O/host_stream.json ;;
+      timeout -k 10 300 python -u tools/host_stream.py --per-call 1024,4096,16384,65536,262144,1048576 \
+          > $O/host_stream.json 2>&1 || rc=$?
+      tail -8 $O/host_stream.json ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
   echo "step $s rc=$rc"

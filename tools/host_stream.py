@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--chunk", type=int, default=1 << 22)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--per-call", default="",
+                    help="comma-separated packets per call: the per-call cost of infw_classify_host on the pinned "
+                         "batch cut into calls of that size")
     args = ap.parse_args()
     import numpy as np
     import infw
@@ -46,8 +49,19 @@ def main():
         best = min(ts)
         out[mode] = {"mpps": round(n / best / 1e6, 1), "s": round(best, 4),
                      "h2d_GB_per_s": round(32 * n / best / 1e9, 1), "d2h_GB_per_s": round(4 * n / best / 1e9, 1)}
-    # the device-resident rate of the same packets, for reference
     print(json.dumps(out), flush=True)
+    for per in [int(x) for x in args.per_call.split(",") if x]:  # (the pinned batch, still registered)
+        parts = [(soa.slice(a, min(n, a + per)), res[a:min(n, a + per)]) for a in range(0, n, per)]
+        for s, r in parts[:4]:
+            clf.classify_host(s, r)
+        best = 1e30
+        for _ in range(args.reps):
+            t = time.perf_counter()
+            for s, r in parts:
+                clf.classify_host(s, r)
+            best = min(best, time.perf_counter() - t)
+        print(json.dumps({"per_call": per, "calls": len(parts), "us_per_call": round(best / len(parts) * 1e6, 1),
+                          "mpps": round(n / best / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
