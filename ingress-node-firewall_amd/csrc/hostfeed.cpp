@@ -11,6 +11,15 @@
 #include <immintrin.h>
 #endif
 
+// The packer's prefetch distance (frames) and store kind (non-temporal or not): build-time knobs for same-box A/Bs
+// of two libraries (tools/hostfeed_ab.sh); the shipped library uses the defaults.
+#ifndef INFW_PACK_PF
+#define INFW_PACK_PF 16
+#endif
+#ifndef INFW_PACK_NT
+#define INFW_PACK_NT 0
+#endif
+
 namespace infw {
 
 void Signal::set(uint64_t v) {
@@ -171,7 +180,7 @@ void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64
             const infw_hostpack_out o{c.out.saddr4 + p, c.out.v6tail + g0 / G * (12 * G) + 12 * rank,
                                       c.mixed ? c.out.ifindex + p : nullptr, c.out.pkt_len + p, c.out.meta + p,
                                       c.out.l4word + p};
-            infw_hostpack_xdp<16, false>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex, o);
+            infw_hostpack_xdp<INFW_PACK_PF, INFW_PACK_NT != 0>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex, o);
             p = e;
         }
     }
