@@ -16,7 +16,7 @@ EXTRA    ?=
 LIB_SRCS := $(SRC)/abi.cpp $(SRC)/image.cpp $(SRC)/tables.cpp $(SRC)/incremental.cpp $(SRC)/controlplane.cpp \
             $(SRC)/hostfeed.cpp $(SRC)/classify.hip $(SRC)/pack.hip $(SRC)/patch.hip
 LIB_OBJS := $(patsubst $(SRC)/%,$(OBJ)/%.o,$(LIB_SRCS))
-HDRS     := include/infw.h $(wildcard $(SRC)/*.h)
+HDRS     := include/infw.h include/infw_host.h $(wildcard $(SRC)/*.h)
 
 all: $(OUT)/libinfw.so $(OUT)/libinfw_workload.so oracle/build/liborc.so $(OUT)/libinfw_loader.so $(OUT)/infw_loader_test
 

@@ -1,6 +1,11 @@
 // hostfeed.cpp — the host packer threads of infw_classify_xdp_host (infw_hostfeed.h).
 #include "infw_hostfeed.h"
 
+#include <errno.h>
+#include <string.h>
+
+#include "../../include/infw_host.h"
+
 #include <sched.h>
 #include <stdio.h>
 
@@ -201,3 +206,31 @@ int host_threads_auto() {
 }
 
 }  // namespace infw
+
+extern "C" int infw_xdp_host_events(const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n,
+                                    uint32_t ifindex, const uint32_t *results, struct infw_event_sample *samples,
+                                    uint64_t cap, uint64_t *count) {
+    if (!count || (n && (!umem || !descs || !results)) || (cap && !samples)) return -EINVAL;
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t r = results[i];
+        if ((r & 0xFFu) != INFW_XDP_DROP) continue;
+        if (k < cap) {
+            infw_event_sample &s = samples[k];
+            const uint32_t len = descs[i].len;
+            const uint32_t captured = len < INFW_MAX_EVENT_DATA ? len : INFW_MAX_EVENT_DATA;
+            s.size = ((8u + captured + 4u + 7u) & ~7u) - 4u;
+            memset(s.raw, 0, sizeof s.raw);
+            event_hdr_st h{};
+            h.ifId = (uint16_t)ifindex;
+            h.ruleId = (uint16_t)(r >> 8);
+            h.action = INFW_XDP_DROP;
+            h.pktLength = (uint16_t)len;
+            memcpy(s.raw, &h, sizeof h);
+            memcpy(s.raw + sizeof h, infw_xdp_frame(umem, descs[i].addr), captured);
+        }
+        k++;
+    }
+    *count = k;
+    return 0;
+}

@@ -155,7 +155,7 @@ ABI_SYMBOLS = [
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
     "infw_table_delete_batch", "infw_set_option", "infw_get_option", "infw_option_name", "infw_classify_variant",
     "infw_kernel_variant_name", "infw_classify_xdp", "infw_classify_xdp_host",
-    "infw_pack_xdp_host", "infw_launch_counts",
+    "infw_pack_xdp_host", "infw_launch_counts", "infw_xdp_host_events",
 ]
 ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
 INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES, INPUT_XDP = 0, 1, 2, 3  # INFW_INPUT_*
@@ -239,6 +239,8 @@ _sig = {
     "infw_classify_variant": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.c_size_t]),
     "infw_kernel_variant_name": (C.c_char_p, [C.c_int]),
     "infw_launch_counts": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
+    "infw_xdp_host_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_uint64, C.POINTER(C.c_uint64)]),
     "infw_classify_xdp": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                     C.c_void_p, C.c_void_p, C.c_void_p]),
     "infw_classify_xdp_host": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64]),

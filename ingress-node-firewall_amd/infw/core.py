@@ -481,6 +481,20 @@ class HostSoa:
         return h
 
 
+def xdp_host_events(umem: np.ndarray, descs: np.ndarray, ifindex: int, results: np.ndarray, cap: int):
+    """Deny-event perf samples of one AF_XDP ring from its frames and result words (infw_xdp_host_events,
+    include/infw_host.h): (cap x 272 uint8 samples, events in the ring — also those past cap)."""
+    n = descs.shape[0]
+    d = np.ascontiguousarray(descs, np.uint32)
+    r = np.ascontiguousarray(results, np.uint32)
+    out = np.zeros((max(cap, 1), N.EVENT_SAMPLE_BYTES), np.uint8)
+    k = C.c_uint64(0)
+    check(N.lib.infw_xdp_host_events(umem.ctypes.data if n else None, d.ctypes.data if n else None, n, ifindex,
+                                     r.ctypes.data if n else None, out.ctypes.data if cap else None, cap, C.byref(k)),
+          "xdp_host_events")
+    return out[:cap], k.value
+
+
 def pack_xdp_host(umem: np.ndarray, descs: np.ndarray, ifindex: int) -> Dict[str, np.ndarray]:
     """infw_pack_xdp_host: the host packer of infw_classify_xdp_host on the calling thread — one AF_XDP ring's frames
     (`descs`: n x 16 B struct xdp_desc over the bytes of `umem`) -> the family-compact streams (numpy, host)."""

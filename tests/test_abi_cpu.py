@@ -1,4 +1,4 @@
-"""C ABI on a CPU-only box: the library loads, exports every symbol include/infw.h
+"""C ABI on a CPU-only box: the library loads, exports every symbol include/*.h
 declares, and its table-map semantics equal the oracle's LPM-trie map
 (update flags / ENOSPC / delete / LPM lookup / get_next_key post-order)."""
 import ctypes as C
@@ -17,7 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    src = open(os.path.join(ROOT, "include", "infw.h")).read()
+    """Every function include/*.h declares (infw.h, infw_host.h)."""
+    inc = os.path.join(ROOT, "include")
+    src = "\n".join(open(os.path.join(inc, f)).read() for f in sorted(os.listdir(inc)) if f.endswith(".h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(infw_\w+)\s*\(", src, flags=re.M)))
 

@@ -223,3 +223,22 @@ def test_xdp_host_optional_outputs(setup):
     clf.classify_xdp_host(args, chunk=512)  # chunks of 512: every chunk boundary inside or between rings
     assert np.array_equal(ver, wver[0]) and np.array_equal(res, want[1])
     assert np.array_equal(clf.stats_read_all(), wst)
+
+
+def test_xdp_host_deny_events_from_device_results(setup):
+    """The host-fed path's deny events (include/infw_host.h infw_xdp_host_events) from the result words the device
+    returned: every ring's perf samples equal the oracle's (kernel.c:392-399) for the same frames, and their number
+    equals the deny counters' packet total."""
+    wl, clf, m = setup
+    rings = rings_of(wl, 60000, [3000, 4000], "unaligned", seed=29)
+    got, _, gst = run_host(clf, rings, 0)
+    total = 0
+    for r, res in zip(rings, got):
+        addr = r["desc"][:, 0].astype(np.uint64) | r["desc"][:, 1].astype(np.uint64) << np.uint64(32)
+        offs = (addr & np.uint64((1 << 48) - 1)) + (addr >> np.uint64(48))
+        _, want = m.collect_event_samples(r["umem"], offs, r["pl"], r["pl"],
+                                          np.full(len(offs), r["ifindex"], np.uint32))
+        samples, k = infw.xdp_host_events(r["umem"], r["desc"], r["ifindex"], res, len(want) + 1)
+        assert k == len(want) and np.array_equal(samples[:k], want)
+        total += k
+    assert total == int(gst[:, 2].sum()) and total > 0  # deny packets counted = events emitted

@@ -111,3 +111,32 @@ def test_pack_arguments():
     o = N.BatchSoaC(None, None, None, None, None, None)
     d = np.zeros((1, 4), np.uint32)
     assert N.lib.infw_pack_xdp_host(umem.ctypes.data, d.ctypes.data, 1, 1, C.byref(o)) == -22
+
+
+@pytest.mark.parametrize("mode", ["aligned", "unaligned"])
+def test_host_events_equal_oracle_samples(mode):
+    """infw_xdp_host_events (include/infw_host.h): the deny-event perf samples of a ring from its frames in host memory
+    and its result words equal the oracle's (kernel.c:392-399: orc_collect_events + orc_perf_sample over the same
+    umem at the descriptors' offsets) byte for byte — header fields, the first min(len, 256) frame bytes, the pad —
+    in ring order; a capacity below the event count keeps the count (perf's lost samples)."""
+    rng = np.random.default_rng(11)
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    m = oracle_for(wl)
+    hdr, cap, pl, ifx = wl.frames(5000, 12000)
+    ifindex = int(np.bincount(ifx).argmax())  # one ring = one interface: that interface's frames
+    hdr, pl = hdr[ifx == ifindex], pl[ifx == ifindex]
+    big = pl.astype(np.uint32)  # frames up to their full length (> 256 B), 80-B snapshots padded with zeros
+    umem, desc = ring(hdr, big, mode, rng)
+    addr = desc[:, 0].astype(np.uint64) | desc[:, 1].astype(np.uint64) << np.uint64(32)
+    offs = (addr & np.uint64((1 << 48) - 1)) + (addr >> np.uint64(48))
+    recs, want = m.collect_event_samples(umem, offs, big, big, np.full(len(offs), ifindex, np.uint32))
+    assert len(recs) > 100
+    # the result words the oracle gives the same frames (what infw_classify_xdp_host returns for this ring)
+    res, _, _, _ = m.classify_frames(np.stack([umem[o:o + 80] for o in offs.astype(np.int64)]), np.minimum(big, 80),
+                                     big, np.full(len(offs), ifindex, np.uint32), nthreads=8)
+    got, k = infw.xdp_host_events(umem, desc, ifindex, res, len(recs) + 5)
+    assert k == len(recs)
+    assert np.array_equal(got[:k], want), np.nonzero((got[:k] != want).any(axis=1))[0][:5]
+    assert not got[k:].any()
+    small, k2 = infw.xdp_host_events(umem, desc, ifindex, res, 10)
+    assert k2 == len(recs) and np.array_equal(small, want[:10])
