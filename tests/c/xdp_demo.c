@@ -24,6 +24,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "infw.h"
+#include "infw_host.h"
 
 #define CHECK(call)                                                                                 \
     do {                                                                                            \
@@ -123,6 +124,15 @@ int main(int argc, char **argv) {
                     l4[0]);
             return 1;
         }
+        /* the event builder needs no device either: result words as a classify would have returned them */
+        const uint32_t words[N] = {INFW_RESULT(INFW_XDP_DROP, 1), INFW_RESULT(INFW_XDP_PASS, 2), 0, 0, 0, 0};
+        struct infw_event_sample ev[1];
+        uint64_t n_ev = 0;
+        CHECK(infw_xdp_host_events(umem, rx, N, 7, words, ev, 1, &n_ev));
+        if (n_ev != 1 || ev[0].size != 108 || memcmp(ev[0].raw + 8, umem + rx[0].addr, 100) != 0) {
+            fprintf(stderr, "host events: %llu events, size %u\n", (unsigned long long)n_ev, ev[0].size);
+            return 1;
+        }
         infw_destroy(ctx);
         printf("xdp_demo OK (host): classify_xdp and classify_xdp_host refused without a device, the host packer "
                "alone packed %d frames, ABI %d\n", N, infw_abi_version());
@@ -203,10 +213,21 @@ int main(int argc, char **argv) {
                 (unsigned long long)allow2_b, (unsigned long long)deny2, (unsigned long long)deny2_b);
         return 1;
     }
+    /* the ring's deny events for the events reader (kernel.c:392-399), built on the host from the frames and the
+     * result words: frame 0 (rule 1, 100 B) is the one denied packet of ring 7 */
+    struct infw_event_sample ev[2];
+    uint64_t n_ev = 0;
+    CHECK(infw_xdp_host_events(umem, rx, N - 1, 7, results, ev, 2, &n_ev));
+    const struct event_hdr_st *eh = (const struct event_hdr_st *)ev[0].raw;
+    if (n_ev != 1 || ev[0].size != ((8 + 100 + 4 + 7) & ~7) - 4 || eh->ifId != 7 || eh->ruleId != 1 || eh->action != 1 ||
+        eh->pktLength != 100 || memcmp(ev[0].raw + 8, umem + rx[0].addr, 100) != 0) {
+        fprintf(stderr, "host events: %llu events, size %u\n", (unsigned long long)n_ev, ev[0].size);
+        return 1;
+    }
     infw_destroy(ctx);
     free(umem), free(rx), free(results), free(verdicts);
     printf("xdp_demo OK: %d frames in 2 rings, allow %llu (%llu B), deny %llu (%llu B); pageable memory refused by the "
-           "device read (-EFAULT) and classified by the host-fed path, ABI %d\n", N,
+           "device read (-EFAULT) and classified by the host-fed path, its deny event built on the host, ABI %d\n", N,
            (unsigned long long)allow, (unsigned long long)allow_b, (unsigned long long)deny,
            (unsigned long long)deny_b, infw_abi_version());
     return 0;
