@@ -3,10 +3,11 @@
  *
  * infw_classify_xdp_host (infw.h) classifies AF_XDP rings whose umem sits in host memory and returns result words,
  * verdicts and per-rule counters.  The reference's program also emits a perf event for every denied packet
- * (bpf/ingress_node_firewall_kernel.c:392-399) that pkg/ebpfsyncer's events reader turns into syslog lines
- * (pkg/events/events.go:77-166).  For frames in HBM the device writes those samples (infw_classify_frames_ex +
- * infw_events_capture); for frames in host memory the daemon already holds every frame, so the samples are built on
- * the host from the ring and the result words — byte for byte the layout infw_events_capture writes.
+ * (bpf/ingress_node_firewall_kernel.c:392-399) that the events reader turns into syslog lines
+ * (pkg/ebpf/ingress_node_firewall_events.go:77-166).  For frames in HBM the device writes those samples
+ * (infw_classify_frames_ex + infw_events_capture); for frames in host memory the daemon already holds every frame, so
+ * the samples are built on the host from the ring and the result words — byte for byte the layout
+ * infw_events_capture writes.
  */
 #ifndef INFW_HOST_H
 #define INFW_HOST_H
