@@ -11,6 +11,7 @@
 #                keys: cfg2 cfg2c cfg1 cfg4 cfg4m cfg2u cfg2d cfg2dw fused cfg3 cfg2w fused80 fused256 fused512 xdphbm frames
 #   lat:<key>    latency-attribution PMC passes of one workload (tools/profile_lat.sh)
 #   micro        tools/micro/gather (random-gather rates by table size; built here beforehand)
+#   commit       commit latency, 1 and 4 device slots, and live swaps mid-stream (tools/commit_latency.py, swap_stream.py)
 #   pcie / hostpack / hoststream   the host-fed feed's microbenchmarks and infw_classify_host (tools/micro, tools/host_stream.py)
 # Output: gpurun_out/<tag>/ (logs); summarise profiles afterwards with tools/summarize_profile.py <tag>_<key>.
 set -u
@@ -95,6 +96,11 @@ step() {
             >> $O/hostpackx.jsonl 2>&1 || { rc=$?; break; }
       done
       tail -12 $O/hostpackx.jsonl ;;
+    commit)   # commit latency at configs[2] scale, one and four device slots (tools/commit_latency.py)
+      timeout -k 10 300 python -u tools/commit_latency.py > $O/commit_latency.jsonl 2>&1 || rc=$?
+      [ $rc -eq 0 ] && { timeout -k 10 300 python -u tools/commit_latency.py --slots 4 > $O/commit_latency_4slots.jsonl 2>&1 || rc=$?; }
+      [ $rc -eq 0 ] && { timeout -k 10 300 python -u tools/swap_stream.py > $O/swap_stream.log 2>&1 || rc=$?; }
+      tail -3 $O/commit_latency.jsonl; tail -4 $O/swap_stream.log ;;
     hoststream) # infw_classify_host: SoA tuples in host memory, chunked H2D / classify / D2H
       timeout -k 10 300 python -u tools/host_stream.py --per-call 1024,4096,16384,65536,262144,1048576 \
           > $O/host_stream.json 2>&1 || rc=$?
