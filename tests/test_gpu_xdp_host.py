@@ -242,3 +242,41 @@ def test_xdp_host_deny_events_from_device_results(setup):
         assert k == len(want) and np.array_equal(samples[:k], want)
         total += k
     assert total == int(gst[:, 2].sum()) and total > 0  # deny packets counted = events emitted
+
+
+def test_xdp_host_two_slots_concurrently(setup):
+    """A daemon with two device slots (both on device 0 here) calls infw_classify_xdp_host from two threads at once,
+    each slot with its own packer pool and pinned slots: every call's words equal the oracle's, and each slot's
+    counters are its own rings' (the per-slot statistics a reader sums like per-CPU slots)."""
+    import threading
+    wl, _, m = setup
+    clf = infw.Classifier(devices=[0, 0], max_entries=wl.n_entries + 16, options={"host_threads": 4})
+    wl.load_into(clf)
+    clf.commit()
+    work = [rings_of(wl, 200000 + 50000 * s, [9000, 7000], "aligned", seed=31 + s) for s in range(2)]
+    want = [oracle_of(m, rs) for rs in work]
+    outs = [[np.full(r["pl"].size, 0xFFFFFFFF, np.uint32) for r in rs] for rs in work]
+    errors = []
+
+    def run(slot):
+        try:
+            for _ in range(5):
+                clf.classify_xdp_host([(r["umem"], r["desc"], r["pl"].size, r["ifindex"], o, None)
+                                       for r, o in zip(work[slot], outs[slot])], chunk=4096, dev=slot)
+        except BaseException as e:  # surfaced below
+            errors.append(e)
+    clf.stats_reset()
+    th = [threading.Thread(target=run, args=(s,)) for s in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for s in range(2):
+        assert all(np.array_equal(g, w) for g, w in zip(outs[s], want[s][0])), s
+    per_rule = [clf.stats_read(rule) for rule in range(1, 100)]
+    for s in range(2):  # slot s counted its own rings five times
+        got = np.array([[p[s].allow_packets, p[s].allow_bytes, p[s].deny_packets, p[s].deny_bytes] for p in per_rule],
+                       np.uint64)
+        assert np.array_equal(got, want[s][2][1:100] * np.uint64(5)), s
+    clf.close()
