@@ -32,6 +32,42 @@ int infw_xdp_host_events(const uint8_t *umem, const struct infw_xdp_desc *descs,
                          const uint32_t *results, struct infw_event_sample *samples, uint64_t cap,
                          uint64_t *count);
 
+/* ------------------------------------------------------------------------ */
+/* DPDK-style bursts (SURVEY.md §8f-3 "AF_XDP/DPDK-style NIC feed"): frames  */
+/* anywhere in host memory, one pointer per frame — an rte_mbuf burst's       */
+/* rte_pktmbuf_mtod(m) with data_len (the first segment's bytes: the linear   */
+/* part the program can read) and pkt_len (the whole frame, every segment:    */
+/* bpf_xdp_get_buff_len) — or frames a capture file or any other source holds. */
+/* One burst = one port = one ifindex.                                        */
+/* ------------------------------------------------------------------------ */
+struct infw_frame_burst {
+    const uint8_t *const *frames;  /* frames[i]: the frame's first byte                            */
+    const uint32_t *linear_len;    /* bytes readable at frames[i] (data_len)                       */
+    const uint32_t *pkt_len;       /* whole-frame length (pkt_len), or NULL: = linear_len          */
+    uint64_t n;
+    uint32_t ifindex;
+    uint32_t flags;                /* 0                                                           */
+    uint32_t *results;             /* n result words, or NULL                                     */
+    uint8_t *verdicts;             /* n XDP verdicts, or NULL                                     */
+};
+/* infw_classify_xdp_host for bursts: the context's packer threads read each  */
+/* frame's header window through its pointer (bytes at or past linear_len[i]  */
+/* read as 0, as kernel.c's data_end checks make them) and the packed tuples  */
+/* are pipelined through the device exactly as for AF_XDP rings (same chunks, */
+/* same options, same results as infw_classify_frames on the same frames).    */
+/* Synchronous; the whole call reads one table epoch.                         */
+int infw_classify_bursts_host(infw_ctx *ctx, int dev, const struct infw_frame_burst *bursts, uint32_t n_bursts,
+                              uint64_t chunk);
+/* The burst packer alone on the calling thread (family-compact streams, as   */
+/* infw_pack_xdp_host writes them; out->ifindex may be NULL).  Pure host.     */
+int infw_pack_burst_host(const struct infw_frame_burst *burst, const struct infw_batch_soa_c_out *out);
+/* Deny-event perf samples of one burst from its result words, as             */
+/* infw_xdp_host_events (captured = min(pkt_len, 256); bytes at or past       */
+/* linear_len — other mbuf segments — written as zeros, as infw_events_capture */
+/* writes them for frames in HBM).  Pure host.  0, or -EINVAL.                */
+int infw_burst_host_events(const struct infw_frame_burst *burst, const uint32_t *results,
+                           struct infw_event_sample *samples, uint64_t cap, uint64_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,6 +169,52 @@ void HostPackPool::work() {
     }
 }
 
+void hostpack_burst(const uint8_t *const *frames, const uint32_t *linear_len, const uint32_t *pkt_len, uint64_t n,
+                    uint32_t ifindex, const infw_hostpack_out &o) {
+    constexpr uint64_t kPF = 16;  // frames ahead (infw_hostpack.h: the headers are DRAM misses)
+    uint32_t rank = 0;
+    uint32_t *tail = nullptr;
+    for (uint64_t i = 0; i < n; i++) {
+        if (i + kPF < n) {
+            __builtin_prefetch(frames[i + kPF] + 10);
+            __builtin_prefetch(frames[i + kPF] + 57);
+        }
+        if ((i & (INFW_V6_GROUP - 1)) == 0) {
+            rank = 0;
+            tail = reinterpret_cast<uint32_t *>(o.v6tail + (i / INFW_V6_GROUP) * (12ull * INFW_V6_GROUP));
+        }
+        const uint8_t *f = frames[i];
+        const uint32_t lin = linear_len[i], plen = pkt_len ? pkt_len[i] : lin;
+        uint32_t s0, s1, s2, s3, l4, meta;
+        if (__builtin_expect(lin >= 58, 1)) {  // every field in place: infw_hostpack_xdp's branch-free form
+            const uint32_t et = (uint32_t)f[12] << 8 | f[13];
+            const bool v4 = et == 0x0800, v6 = et == 0x86DD;
+            const uint32_t ip = (v4 || v6) ? ~0u : 0u;
+            const uint32_t proto = f[v6 ? 20 : 23] & ip;
+            s0 = infw_ld32(f + (v6 ? 22 : 26)) & ip;
+            l4 = infw_ld32(f + (v6 ? 54 : 34)) & ip;
+            s1 = infw_ld32(f + 26);
+            s2 = infw_ld32(f + 30);
+            s3 = infw_ld32(f + 34);
+            meta = et | proto << 16 | (lin > 255u ? 255u : lin) << 24;
+        } else {
+            infw_tuple t;
+            infw_pack_header(f, lin, plen, ifindex, &t);
+            s0 = t.saddr[0], s1 = t.saddr[1], s2 = t.saddr[2], s3 = t.saddr[3];
+            l4 = t.l4word;
+            meta = t.meta;
+        }
+        const bool is6 = (meta & 0xFFFFu) == 0x86DDu;
+        tail[3 * rank] = s1, tail[3 * rank + 1] = s2, tail[3 * rank + 2] = s3;
+        rank += is6;
+        o.saddr4[i] = s0;
+        if (o.ifindex) o.ifindex[i] = ifindex;
+        o.pkt_len[i] = plen;
+        o.meta[i] = meta;
+        o.l4word[i] = l4;
+    }
+}
+
 void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64_t a, uint64_t b) {
     constexpr uint64_t G = INFW_V6_GROUP;
     for (uint32_t si = c.seg0; si < c.seg1; si++) {
@@ -185,7 +231,12 @@ void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64
             const infw_hostpack_out o{c.out.saddr4 + p, c.out.v6tail + g0 / G * (12 * G) + 12 * rank,
                                       c.mixed ? c.out.ifindex + p : nullptr, c.out.pkt_len + p, c.out.meta + p,
                                       c.out.l4word + p};
-            infw_hostpack_xdp<INFW_PACK_PF, INFW_PACK_NT != 0>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex, o);
+            if (s.frames)
+                hostpack_burst(s.frames + (p - s.pos), s.linear_len + (p - s.pos),
+                               s.pkt_len ? s.pkt_len + (p - s.pos) : nullptr, e - p, s.ifindex, o);
+            else
+                infw_hostpack_xdp<INFW_PACK_PF, INFW_PACK_NT != 0>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex,
+                                                                   o);
             p = e;
         }
     }
@@ -209,26 +260,61 @@ int host_threads_auto() {
 
 extern "C" int infw_xdp_host_events(const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n,
                                     uint32_t ifindex, const uint32_t *results, struct infw_event_sample *samples,
+                                    uint64_t cap, uint64_t *count);
+
+// Shared by the two event builders: sample k of a denied packet (kernel.c:392-399, infw_events_capture's layout).
+static void infw_fill_sample(infw_event_sample &s, const uint8_t *f, uint32_t linear, uint32_t plen, uint32_t ifindex,
+                             uint32_t r) {
+    const uint32_t captured = plen < INFW_MAX_EVENT_DATA ? plen : INFW_MAX_EVENT_DATA;
+    s.size = ((8u + captured + 4u + 7u) & ~7u) - 4u;
+    memset(s.raw, 0, sizeof s.raw);
+    event_hdr_st h{};
+    h.ifId = (uint16_t)ifindex;
+    h.ruleId = (uint16_t)(r >> 8);
+    h.action = INFW_XDP_DROP;
+    h.pktLength = (uint16_t)plen;
+    memcpy(s.raw, &h, sizeof h);
+    memcpy(s.raw + sizeof h, f, captured < linear ? captured : linear);  // past the linear part: zeros
+}
+
+extern "C" int infw_burst_host_events(const struct infw_frame_burst *b, const uint32_t *results,
+                                      struct infw_event_sample *samples, uint64_t cap, uint64_t *count) {
+    if (!b || !count || (b->n && (!b->frames || !b->linear_len || !results)) || (cap && !samples)) return -EINVAL;
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < b->n; i++) {
+        if ((results[i] & 0xFFu) != INFW_XDP_DROP) continue;
+        if (k < cap)
+            infw_fill_sample(samples[k], b->frames[i], b->linear_len[i], b->pkt_len ? b->pkt_len[i] : b->linear_len[i],
+                             b->ifindex, results[i]);
+        k++;
+    }
+    *count = k;
+    return 0;
+}
+
+extern "C" int infw_pack_burst_host(const struct infw_frame_burst *b, const struct infw_batch_soa_c_out *out) {
+    if (!b || !out) return -EINVAL;
+    if (b->n == 0) return 0;
+    bool ok = b->frames && b->linear_len && out->saddr4 && out->v6tail && out->pkt_len && out->meta && out->l4word;
+    for (const void *q : {(const void *)out->saddr4, (const void *)out->v6tail, (const void *)out->ifindex,
+                          (const void *)out->pkt_len, (const void *)out->meta, (const void *)out->l4word})
+        ok = ok && ((uintptr_t)q & 3) == 0;
+    if (!ok) return -EINVAL;
+    infw::hostpack_burst(b->frames, b->linear_len, b->pkt_len, b->n, b->ifindex,
+                         {out->saddr4, out->v6tail, out->ifindex, out->pkt_len, out->meta, out->l4word});
+    return 0;
+}
+
+extern "C" int infw_xdp_host_events(const uint8_t *umem, const struct infw_xdp_desc *descs, uint64_t n,
+                                    uint32_t ifindex, const uint32_t *results, struct infw_event_sample *samples,
                                     uint64_t cap, uint64_t *count) {
     if (!count || (n && (!umem || !descs || !results)) || (cap && !samples)) return -EINVAL;
     uint64_t k = 0;
     for (uint64_t i = 0; i < n; i++) {
-        const uint32_t r = results[i];
-        if ((r & 0xFFu) != INFW_XDP_DROP) continue;
-        if (k < cap) {
-            infw_event_sample &s = samples[k];
-            const uint32_t len = descs[i].len;
-            const uint32_t captured = len < INFW_MAX_EVENT_DATA ? len : INFW_MAX_EVENT_DATA;
-            s.size = ((8u + captured + 4u + 7u) & ~7u) - 4u;
-            memset(s.raw, 0, sizeof s.raw);
-            event_hdr_st h{};
-            h.ifId = (uint16_t)ifindex;
-            h.ruleId = (uint16_t)(r >> 8);
-            h.action = INFW_XDP_DROP;
-            h.pktLength = (uint16_t)len;
-            memcpy(s.raw, &h, sizeof h);
-            memcpy(s.raw + sizeof h, infw_xdp_frame(umem, descs[i].addr), captured);
-        }
+        if ((results[i] & 0xFFu) != INFW_XDP_DROP) continue;
+        if (k < cap)  // a single-buffer AF_XDP frame: linear = frame length = the descriptor's len
+            infw_fill_sample(samples[k], infw_xdp_frame(umem, descs[i].addr), descs[i].len, descs[i].len, ifindex,
+                             results[i]);
         k++;
     }
     *count = k;

@@ -41,13 +41,20 @@ class Signal {
     std::condition_variable cv_;
 };
 
-// One ring's run of descriptors inside a chunk, at chunk positions [pos, pos + n).
+// One ring's run of descriptors inside a chunk, at chunk positions [pos, pos + n): an AF_XDP ring's (umem +
+// descriptors) or a burst's (frame pointers + linear and frame lengths; frames != nullptr).
 struct XdpSeg {
     const uint8_t *umem;
     const infw_xdp_desc *descs;
     uint64_t n, pos;
     uint32_t ifindex;
+    const uint8_t *const *frames = nullptr;
+    const uint32_t *linear_len = nullptr, *pkt_len = nullptr;
 };
+
+// A burst's frames [0, n) -> the family-compact streams (host code; the burst form of infw_hostpack_xdp).
+void hostpack_burst(const uint8_t *const *frames, const uint32_t *linear_len, const uint32_t *pkt_len, uint64_t n,
+                    uint32_t ifindex, const infw_hostpack_out &o);
 
 // A chunk: segments [seg0, seg1) of the call's segment list, n descriptors in all.  `mixed`: its segments carry more
 // than one ifindex, so the packers write the ifindex stream (else the device fills it).  `out`: the chunk's streams in

@@ -101,6 +101,12 @@ class XdpRing(C.Structure):
                 ("flags", C.c_uint32), ("results", C.c_void_p), ("verdicts", C.c_void_p)]
 
 
+class FrameBurst(C.Structure):
+    """struct infw_frame_burst (include/infw_host.h): a DPDK-style burst of frames in host memory, one pointer each."""
+    _fields_ = [("frames", C.c_void_p), ("linear_len", C.c_void_p), ("pkt_len", C.c_void_p), ("n", C.c_uint64),
+                ("ifindex", C.c_uint32), ("flags", C.c_uint32), ("results", C.c_void_p), ("verdicts", C.c_void_p)]
+
+
 class EventHdrSt(C.Structure):
     """struct event_hdr_st (ingress_node_firewall.h:58-64), 8 B packed."""
     _pack_ = 1
@@ -155,7 +161,8 @@ ABI_SYMBOLS = [
     "infw_get_launch", "infw_events_capture", "infw_build_id", "infw_table_export", "infw_table_import",
     "infw_table_delete_batch", "infw_set_option", "infw_get_option", "infw_option_name", "infw_classify_variant",
     "infw_kernel_variant_name", "infw_classify_xdp", "infw_classify_xdp_host",
-    "infw_pack_xdp_host", "infw_launch_counts", "infw_xdp_host_events",
+    "infw_pack_xdp_host", "infw_launch_counts", "infw_xdp_host_events", "infw_classify_bursts_host",
+    "infw_pack_burst_host", "infw_burst_host_events",
 ]
 ABI_VERSION = 4  # include/infw.h INFW_ABI_VERSION
 INPUT_SOA, INPUT_COMPACT, INPUT_FRAMES, INPUT_XDP = 0, 1, 2, 3  # INFW_INPUT_*
@@ -241,6 +248,9 @@ _sig = {
     "infw_launch_counts": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "infw_xdp_host_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p,
                                        C.c_uint64, C.POINTER(C.c_uint64)]),
+    "infw_classify_bursts_host": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64]),
+    "infw_pack_burst_host": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "infw_burst_host_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "infw_classify_xdp": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                     C.c_void_p, C.c_void_p, C.c_void_p]),
     "infw_classify_xdp_host": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64]),

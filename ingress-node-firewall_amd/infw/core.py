@@ -362,6 +362,15 @@ class Classifier:
             arr[i] = N.XdpRing(ptr(umem), ptr(descs), n, ifindex, 0, ptr(results), ptr(verdicts))
         check(N.lib.infw_classify_xdp_host(self._ctx, dev, arr, len(rings), chunk), "classify_xdp_host")
 
+    def classify_bursts_host(self, bursts, chunk: int = 0, dev: int = 0) -> None:
+        """infw_classify_bursts_host (include/infw_host.h): DPDK-style bursts of frames in host memory — per burst a
+        `Burst` (frame pointers, linear and frame lengths, ifindex, optional result / verdict arrays) — packed on the
+        context's host threads and classified through the device (synchronous)."""
+        arr = (N.FrameBurst * max(1, len(bursts)))()
+        for i, b in enumerate(bursts):
+            arr[i] = b.c()
+        check(N.lib.infw_classify_bursts_host(self._ctx, dev, arr, len(bursts), chunk), "classify_bursts_host")
+
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
         """The perf samples of the deny events classify_events wrote (kernel.c:392-399) from the frames the batch was
@@ -479,6 +488,46 @@ class HostSoa:
         h.saddr, h.ifindex, h.pkt_len = self.saddr[a:b], self.ifindex[a:b], self.pkt_len[a:b]
         h.meta, h.l4word = self.meta[a:b], self.l4word[a:b]
         return h
+
+
+class Burst:
+    """struct infw_frame_burst: frames given as host addresses (uint64 array, e.g. rte_pktmbuf_mtod of each mbuf),
+    their linear lengths (data_len) and frame lengths (pkt_len; None: the linear lengths), one ifindex; results /
+    verdicts: numpy arrays to fill, or None.  Keeps its arrays alive while the C struct points at them."""
+
+    def __init__(self, frames: np.ndarray, linear_len: np.ndarray, pkt_len: Optional[np.ndarray], ifindex: int,
+                 results: Optional[np.ndarray] = None, verdicts: Optional[np.ndarray] = None):
+        self.frames = np.ascontiguousarray(frames, np.uint64)
+        self.linear_len = np.ascontiguousarray(linear_len, np.uint32)
+        self.pkt_len = None if pkt_len is None else np.ascontiguousarray(pkt_len, np.uint32)
+        self.n, self.ifindex, self.results, self.verdicts = self.frames.size, ifindex, results, verdicts
+
+    def c(self) -> "N.FrameBurst":
+        ptr = lambda a: None if a is None or a.size == 0 else a.ctypes.data  # noqa: E731
+        return N.FrameBurst(ptr(self.frames), ptr(self.linear_len), ptr(self.pkt_len), self.n, self.ifindex, 0,
+                            ptr(self.results), ptr(self.verdicts))
+
+
+def pack_burst_host(burst: Burst) -> Dict[str, np.ndarray]:
+    """infw_pack_burst_host: a burst's frames -> the family-compact streams on the calling thread (numpy, host)."""
+    n = burst.n
+    out = {k: np.zeros(max(n, 1), np.uint32) for k in ("saddr4", "ifindex", "pkt_len", "meta", "l4word")}
+    out["v6tail"] = np.zeros(max(1, (n + 63) // 64) * 768, np.uint8)
+    o = N.BatchSoaC(*(out[k].ctypes.data for k in ("saddr4", "v6tail", "ifindex", "pkt_len", "meta", "l4word")))
+    b = burst.c()
+    check(N.lib.infw_pack_burst_host(C.byref(b), C.byref(o)), "pack_burst_host")
+    return {k: v[:n] if k != "v6tail" else v for k, v in out.items()}
+
+
+def burst_host_events(burst: Burst, results: np.ndarray, cap: int):
+    """Deny-event perf samples of a burst from its result words (infw_burst_host_events): (cap x 272 uint8, count)."""
+    r = np.ascontiguousarray(results, np.uint32)
+    out = np.zeros((max(cap, 1), N.EVENT_SAMPLE_BYTES), np.uint8)
+    k = C.c_uint64(0)
+    b = burst.c()
+    check(N.lib.infw_burst_host_events(C.byref(b), r.ctypes.data if r.size else None,
+                                       out.ctypes.data if cap else None, cap, C.byref(k)), "burst_host_events")
+    return out[:cap], k.value
 
 
 def xdp_host_events(umem: np.ndarray, descs: np.ndarray, ifindex: int, results: np.ndarray, cap: int):

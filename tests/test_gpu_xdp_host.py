@@ -280,3 +280,34 @@ def test_xdp_host_two_slots_concurrently(setup):
                        np.uint64)
         assert np.array_equal(got, want[s][2][1:100] * np.uint64(5)), s
     clf.close()
+
+
+@pytest.mark.parametrize("chunk", [512, 0])
+def test_bursts_host_match_oracle(setup, chunk):
+    """infw_classify_bursts_host (include/infw_host.h): DPDK-style bursts — one pointer per frame, first segments
+    shorter than the frame for most, one port per burst, ragged sizes — give the oracle's result words, verdicts and
+    counters for the same frames (linear length = the first segment's, frame length = the whole frame's)."""
+    from test_hostpack_cpu import _burst_of
+    wl, clf, m = setup
+    hdr, cap, pl, ifx = wl.frames(300000 + chunk, 30000)
+    rng = np.random.default_rng(41 + chunk)
+    cap = np.minimum(cap, rng.choice(np.array([60, 64, 128, 30, 9000], np.uint32), cap.size,
+                                     p=[.3, .3, .2, .05, .15])).astype(np.uint32)
+    bursts, keep, want_r, want_v = [], [], [], []
+    for port, size in zip(np.unique(ifx)[:3], [1, 4097, 9000]):
+        idx = np.nonzero(ifx == port)[0][:size]
+        buf, b, _ = _burst_of(hdr[idx], cap[idx], pl[idx], int(port))
+        b.results = np.full(idx.size, 0xFFFFFFFF, np.uint32)
+        b.verdicts = np.full(idx.size, 7, np.uint8)
+        bursts.append(b)
+        keep.append(buf)
+        r, v, _, _ = m.classify_frames(hdr[idx], cap[idx], pl[idx], ifx[idx], nthreads=8)
+        want_r.append(r)
+        want_v.append(v)
+    allidx = np.concatenate([np.nonzero(ifx == port)[0][:size] for port, size in zip(np.unique(ifx)[:3], [1, 4097, 9000])])
+    _, _, wst, _ = m.classify_frames(hdr[allidx], cap[allidx], pl[allidx], ifx[allidx], nthreads=8)
+    clf.stats_reset()
+    clf.classify_bursts_host(bursts, chunk=chunk)
+    for b, r, v in zip(bursts, want_r, want_v):
+        assert np.array_equal(b.results, r) and np.array_equal(b.verdicts, v)
+    assert np.array_equal(clf.stats_read_all(), wst)

@@ -140,3 +140,79 @@ def test_host_events_equal_oracle_samples(mode):
     assert not got[k:].any()
     small, k2 = infw.xdp_host_events(umem, desc, ifindex, res, 10)
     assert k2 == len(recs) and np.array_equal(small, want[:10])
+
+
+def _burst_of(hdr, linear, pkt_len, ifindex, stride=2048):
+    """A DPDK-style burst: each frame's snapshot at its own place in a buffer (zeros after it), one pointer per frame."""
+    n = len(hdr)
+    buf = np.zeros(n * stride + 512, np.uint8)
+    for i in range(n):
+        h = np.frombuffer(bytes(hdr[i]), np.uint8)
+        buf[i * stride: i * stride + h.size] = h
+    ptrs = buf.ctypes.data + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    return buf, infw.Burst(ptrs, linear, pkt_len, ifindex), np.arange(n, dtype=np.uint64) * np.uint64(stride)
+
+
+def test_burst_packs_walk_to_oracle():
+    """infw_pack_burst_host: frames behind pointers with linear lengths below their frame lengths (multi-segment mbufs)
+    pack to tuples that the compiled host image walks to the oracle's result words for the same frames."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    n = 5 * 64 + 13
+    hdr, cap, pl, ifx = wl.frames(777, n)
+    port = int(np.bincount(ifx).argmax())
+    # first segments of 60 / 64 / 128 B (the rest of the frame in other segments), a few cut inside the headers
+    rng = np.random.default_rng(19)
+    cap = np.minimum(cap, rng.choice(np.array([60, 64, 128, 20, 41, 9000], np.uint32), n,
+                                     p=[.3, .3, .2, .05, .05, .1])).astype(np.uint32)
+    want, _, _, _ = oracle_for(wl).classify_frames(hdr, cap, pl, np.full(n, port, np.uint32), nthreads=4)
+    assert (cap < pl).mean() > 0.5  # linear part shorter than the frame for most of them
+    buf, b, _ = _burst_of(hdr, cap, pl, port)
+    c = infw.pack_burst_host(b)
+    assert (c["ifindex"] == port).all() and np.array_equal(c["pkt_len"], pl)
+    clf = infw.Classifier(flags=infw.F_HOST_ONLY, max_entries=wl.n_entries + 16)
+    wl.load_into(clf)
+    clf.commit()
+    got = clf.debug_walk(infw.compact_to_tuples(c))
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:5], got[bad[:5]], want[bad[:5]])
+
+
+def test_burst_edge_frames_pack_to_kernel_fields():
+    """Every truncation 0..60 of several protocols as the linear part of a 1514-B frame: the packed fields are the
+    bytes kernel.c reads within the linear part, pkt_len the whole frame's."""
+    base = [frame("10.1.2.3", "192.0.2.9", "tcp", dport=8080, length=64),
+            frame("2001:db8::5", "2001:db8::1", "udp", dport=53, length=80),
+            frame("2001:db8::7", proto="icmpv6", icmp_type=128, icmp_code=0),
+            frame("10.1.1.1", "192.0.2.9", "tcp", dport=22, ethertype=0x0806)]
+    frames, lens = [], []
+    for f in base:
+        for L in range(0, 61):
+            frames.append(np.frombuffer(bytes(f).ljust(80, b"\0")[:80], np.uint8))
+            lens.append(L)
+    lens = np.array(lens, np.uint32)
+    buf, b, _ = _burst_of(frames, lens, np.full(len(lens), 1514, np.uint32), 3)
+    t = infw.compact_to_tuples(infw.pack_burst_host(b))
+    for i, L in enumerate(lens):
+        s, meta, l4 = fields_ref(bytes(frames[i]), int(L))
+        assert t[i, 6] == meta and t[i, 7] == l4 and t[i, 5] == 1514 and t[i, 0] == s[0], (i, L)
+        if (meta & 0xFFFF) == 0x86DD:
+            assert np.array_equal(t[i, 1:4], s[1:4]), (i, L)
+
+
+def test_burst_events_equal_oracle_samples():
+    """infw_burst_host_events: the perf samples of a burst's denied frames equal the oracle's — captured =
+    min(pkt_len, 256) with zeros past the linear part — and the count survives a small capacity."""
+    wl = W.Workload(W.CFG2_MIXED_1M, n_prefixes=20000, n_templates=64)
+    m = oracle_for(wl)
+    hdr, cap, pl, ifx = wl.frames(9000, 8000)
+    port = int(np.bincount(ifx).argmax())
+    hdr, cap, pl = hdr[ifx == port], cap[ifx == port], pl[ifx == port]
+    cap = np.minimum(cap, np.where(np.arange(cap.size) % 3 == 0, 64, 9000)).astype(np.uint32)  # some 64-B first segments
+    buf, b, offs = _burst_of(hdr, cap, pl, port)
+    recs, want = m.collect_event_samples(buf, offs, cap, pl, np.full(len(offs), port, np.uint32))
+    res, _, _, _ = m.classify_frames(hdr, cap, pl, np.full(len(offs), port, np.uint32), nthreads=8)
+    assert len(recs) > 50
+    got, k = infw.burst_host_events(b, res, len(recs) + 3)
+    assert k == len(recs) and np.array_equal(got[:k], want) and not got[k:].any()
+    small, k2 = infw.burst_host_events(b, res, 7)
+    assert k2 == k and np.array_equal(small, want[:7])
