@@ -60,7 +60,8 @@ ALGO_BYTES_PER_PKT = 36  # standard layout: 32 B SoA tuple in + 4 B result word 
 # family-compact layout (infw_batch_soa_c): 4 address bytes per packet + 12 more per IPv6 packet, + 16 B of
 # ifindex/pkt_len/meta/l4word in, + 4 B result word out = 24 + 12 * (IPv6 share) bytes per packet
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md)
-PCIE_H2D_GBS = 56.9      # dense pinned H2D copy rate, PCIe Gen5 x16 (tools/micro/pcie.hip, profiles/r06a/pcie.jsonl)
+PCIE_H2D_GBS = 56.9      # dense pinned H2D copy rate, PCIe Gen5 x16 (tools/micro/pcie.hip, profiles/r06z/micro/pcie.jsonl)
+HOST_FED = ("host-packed", "host-bursts")  # --xdp-ring feeds whose frames the library's host packer threads read
 METRIC = "Mpps classified @1M prefixes x 100 rules, 1/2/4/8 GPUs; % HBM BW roofline"
 
 
@@ -180,14 +181,19 @@ def parse(argv=None):
                     help="with --in-process: every slot on device 0 (rehearsal of the N-slot shape on one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="per-context option (include/infw.h) for every context this bench creates")
-    ap.add_argument("--xdp-ring", choices=("hbm", "host", "registered", "host-packed"), default=None,
+    ap.add_argument("--xdp-ring", choices=("hbm", "host", "registered", "host-packed", "host-bursts"), default=None,
                     help="AF_XDP feed: the frames in a umem of 2048-B chunks (--from-frames sets another chunk size) "
                          "in HBM, in pinned host memory (hipHostMalloc) or in the process's own anonymous mapping "
                          "page-locked with infw_host_register (what a daemon's XDP_UMEM_REG memory is), read over "
                          "PCIe; one RX descriptor ring per interface, classified by infw_classify_xdp (implies --fused). "
                          "host-packed: umem and rings in the process's own pageable mapping, read by the library's "
                          "host packer threads, the packed tuples pipelined through the device "
-                         "(infw_classify_xdp_host); result words into pinned host memory")
+                         "(infw_classify_xdp_host); result words into pinned host memory. host-bursts: the same frames "
+                         "handed over DPDK-style, one pointer per frame with its data_len / pkt_len "
+                         "(infw_classify_bursts_host, include/infw_host.h)")
+    ap.add_argument("--burst-size", type=int, default=0,
+                    help="with --xdp-ring host-bursts: frames per burst (e.g. 32, an rte_eth_rx_burst's; 0: one burst "
+                         "per interface)")
     ap.add_argument("--umem-order", choices=("packet", "ring"), default=None,
                     help="AF_XDP umem layout: frames at their packet index (rings interleave: default for hbm/host/"
                          "registered) or each ring's frames back to back in arrival order (a socket's own umem fed by a "
@@ -201,7 +207,7 @@ def parse(argv=None):
     if args.xdp_ring:
         args.from_frames = args.from_frames or 2048
         args.fused = True
-        args.umem_order = args.umem_order or ("ring" if args.xdp_ring == "host-packed" else "packet")
+        args.umem_order = args.umem_order or ("ring" if args.xdp_ring in HOST_FED else "packet")
         if args.batch == 1 << 27:
             args.batch = 1 << 24  # 16M frames x 2048 B = 32 GiB of umem
     args.options = {}
@@ -509,12 +515,13 @@ def run_rank(args):
         # umem order: "packet" — every frame at its packet index (the interfaces' rings interleave in one umem, so a
         # ring's addresses ascend with gaps); "ring" — each ring's frames back to back in arrival order, as a socket's
         # own umem holds them in steady state when its fill ring returns chunks in the order they were consumed
-        order, at = [], 0
+        order, ring_addrs, at = [], [], 0
         for ifv in np.unique(ifx_h):
             idx = np.nonzero(ifx_h == ifv)[0]
             d = np.zeros((len(idx), 4), np.uint32)
             slots = idx.astype(np.uint64) if args.umem_order == "packet" else np.arange(at, at + len(idx), dtype=np.uint64)
             a = slots * np.uint64(stride)
+            ring_addrs.append(a)
             d[:, 0], d[:, 1], d[:, 2] = a & np.uint64(0xFFFFFFFF), a >> np.uint64(32), len_h[idx]
             rings.append([int(ifv), len(idx), torch.from_numpy(d.view(np.int32))])
             order.append(idx)
@@ -548,7 +555,7 @@ def run_rank(args):
                 t = own(r[2].numel() * 4).view(torch.int32)
                 t.copy_(r[2].view(-1))
                 r[2] = t
-        elif args.xdp_ring == "host-packed":
+        elif args.xdp_ring in HOST_FED:
             # the daemon's own pageable memory (an anonymous mapping, huge pages requested as AF_XDP umems commonly
             # are), never registered: the library's packer threads read it on the CPU; the rings stay pageable too
             import mmap
@@ -564,6 +571,26 @@ def run_rank(args):
             frames = umem
             host_res = [torch.empty(max(r[1], 1), dtype=torch.int32).pin_memory()[:r[1]] for r in rings]
             ring_args = [(frames, d, nr, ifv, hr, None) for (ifv, nr, d), hr in zip(rings, host_res)]
+            if args.xdp_ring == "host-bursts":
+                # DPDK-style: per frame its address (rte_pktmbuf_mtod), data_len (the linear part) and pkt_len, cut
+                # into bursts of --burst-size frames of one port each (0: one burst per interface)
+                flen_h = f_len[:n].cpu().numpy().view(np.uint32)
+                base = np.uint64(frames.data_ptr())
+                bursts = []
+                for (ifv, nr, d), hr, idx, a in zip(rings, host_res, order, ring_addrs):
+                    ptrs, hres = base + a, hr.numpy().view(np.uint32)
+                    bs = args.burst_size or max(nr, 1)
+                    for lo in range(0, nr, bs):
+                        hi = min(nr, lo + bs)
+                        bursts.append(infw.Burst(ptrs[lo:hi], lin_h[idx[lo:hi]], flen_h[idx[lo:hi]], ifv,
+                                                 results=hres[lo:hi]))
+                bursts = infw.BurstArray(bursts)  # the C array a daemon would hand over, built once (untimed)
+
+            def host_call():
+                if args.xdp_ring == "host-bursts":
+                    clf.classify_bursts_host(bursts, chunk=args.xdp_chunk)
+                else:
+                    clf.classify_xdp_host(ring_args, chunk=args.xdp_chunk)
         else:
             for r in rings:
                 r[2] = r[2].to(dev)
@@ -572,8 +599,8 @@ def run_rank(args):
         ref = torch.empty_like(results)
         clf.classify_c(batch_c, results=ref)
         off = 0
-        if args.xdp_ring == "host-packed":
-            clf.classify_xdp_host(ring_args, chunk=args.xdp_chunk)
+        if args.xdp_ring in HOST_FED:
+            host_call()
             results.copy_(torch.cat(host_res).to(dev))
         else:
             for ifv, nr, d in rings:
@@ -600,11 +627,11 @@ def run_rank(args):
         clf.stats_bind(0, stats.data_ptr())
         if ev is not None:
             ev[0].record(stream)
-        if args.xdp_ring == "host-packed":  # synchronous: pack || H2D || classify || D2H inside the library
+        if args.xdp_ring in HOST_FED:  # synchronous: pack || H2D || classify || D2H inside the library
             if ev is not None:
                 ev[2].record(stream)
             t0 = time.perf_counter()
-            clf.classify_xdp_host(ring_args, chunk=args.xdp_chunk)
+            host_call()
             step_wall.append(time.perf_counter() - t0)
         elif args.xdp_ring:
             if ev is not None:
@@ -653,7 +680,7 @@ def run_rank(args):
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    if args.xdp_ring == "host-packed":  # the library's own streams: the step's wall time stands for the kernel's
+    if args.xdp_ring in HOST_FED:  # the library's own streams: the step's wall time stands for the kernel's
         kern_ms = [w * 1e3 for w in step_wall[-args.steps:]]
     elif args.from_frames:  # ev[0] -> pack -> ev[2] -> classify -> ev[1]
         pack_ms = [e[0].elapsed_time(e[2]) for e in evs]
@@ -680,11 +707,11 @@ def run_rank(args):
         assert torch.equal(total, digest_block * args.steps), "a timed step's counters differ from the warmup's"
     digest = stats_digest(digest_block.cpu().numpy())
     # the registry name of the instantiation(s) this line ran (infw_classify_variant: the library's own selector)
-    kernel = clf.variant(infw.INPUT_COMPACT if args.xdp_ring == "host-packed" else infw.INPUT_XDP if args.xdp_ring else
+    kernel = clf.variant(infw.INPUT_COMPACT if args.xdp_ring in HOST_FED else infw.INPUT_XDP if args.xdp_ring else
                          {"standard": infw.INPUT_SOA, "compact": infw.INPUT_COMPACT,
                           "frames": infw.INPUT_FRAMES}[args.layout])
     host_feed = None
-    if args.xdp_ring == "host-packed":
+    if args.xdp_ring in HOST_FED:
         # per step over PCIe, as infw_classify_xdp_host cuts the rings: chunks of at most C descriptors running on
         # from one ring into the next (chunk 0: 512K, or a quarter of a call under four of those, >= 32K); a chunk of
         # n descriptors is one H2D copy of 28 B x S (S = n rounded up to 64: saddr4, pkt_len, meta, l4word and the
@@ -733,7 +760,14 @@ def run_rank(args):
                                                       "library's packer threads on the CPU; packed tuples to the "
                                                       "device and result words back over PCIe (PCIe-inclusive "
                                                       "rate; kernel_ms_avg is the step's wall time)",
+                                       "host-bursts": "the process's own pageable anonymous mapping, handed over "
+                                                      "as DPDK-style bursts (a pointer, data_len and pkt_len per "
+                                                      "frame) and read by the library's packer threads; packed "
+                                                      "tuples to the device and result words back over PCIe "
+                                                      "(PCIe-inclusive rate; kernel_ms_avg is the step's wall time)",
                                        "hbm": "HBM"}[args.xdp_ring],
+                                   **({"bursts": bursts.n, "burst_size": args.burst_size or None}
+                                      if args.xdp_ring == "host-bursts" else {}),
                                    **({"host_feed": host_feed} if host_feed else {})}}
     elif args.fused:
         extra_pipe = {"from_frames": {"frame_stride": stride, "fused": True,

@@ -217,7 +217,13 @@ void hostpack_burst(const uint8_t *const *frames, const uint32_t *linear_len, co
 
 void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64_t a, uint64_t b) {
     constexpr uint64_t G = INFW_V6_GROUP;
-    for (uint32_t si = c.seg0; si < c.seg1; si++) {
+    // the segment holding descriptor a (positions ascend within a chunk; a chunk of bursts may hold thousands)
+    uint32_t first = c.seg0;
+    if (c.seg1 - c.seg0 > 8)
+        first = (uint32_t)(std::upper_bound(segs.begin() + c.seg0, segs.begin() + c.seg1, a,
+                                            [](uint64_t v, const XdpSeg &g) { return v < g.pos; }) -
+                           segs.begin()) - 1;
+    for (uint32_t si = first; si < c.seg1 && segs[si].pos < b; si++) {
         const XdpSeg &s = segs[si];
         const uint64_t s0 = std::max(a, s.pos), s1 = std::min(b, s.pos + s.n);
         for (uint64_t p = s0; p < s1;) {
@@ -231,6 +237,15 @@ void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64
             const infw_hostpack_out o{c.out.saddr4 + p, c.out.v6tail + g0 / G * (12 * G) + 12 * rank,
                                       c.mixed ? c.out.ifindex + p : nullptr, c.out.pkt_len + p, c.out.meta + p,
                                       c.out.l4word + p};
+            if (s.frames && p == s0 && si + 1 < c.seg1 && segs[si + 1].frames) {
+                // a burst's first frames are not prefetched by its own loop (which runs 16 frames ahead of itself):
+                // issue them while this segment packs, so rx_burst-sized bursts keep as many misses in flight
+                const XdpSeg &nx = segs[si + 1];
+                for (uint64_t q = 0, m = std::min<uint64_t>(nx.n, 16); q < m; q++) {
+                    __builtin_prefetch(nx.frames[q] + 10);
+                    __builtin_prefetch(nx.frames[q] + 57);
+                }
+            }
             if (s.frames)
                 hostpack_burst(s.frames + (p - s.pos), s.linear_len + (p - s.pos),
                                s.pkt_len ? s.pkt_len + (p - s.pos) : nullptr, e - p, s.ifindex, o);

@@ -365,11 +365,10 @@ class Classifier:
     def classify_bursts_host(self, bursts, chunk: int = 0, dev: int = 0) -> None:
         """infw_classify_bursts_host (include/infw_host.h): DPDK-style bursts of frames in host memory — per burst a
         `Burst` (frame pointers, linear and frame lengths, ifindex, optional result / verdict arrays) — packed on the
-        context's host threads and classified through the device (synchronous)."""
-        arr = (N.FrameBurst * max(1, len(bursts)))()
-        for i, b in enumerate(bursts):
-            arr[i] = b.c()
-        check(N.lib.infw_classify_bursts_host(self._ctx, dev, arr, len(bursts), chunk), "classify_bursts_host")
+        context's host threads and classified through the device (synchronous).  `bursts`: a list of Burst, or a
+        BurstArray built once (the C array a daemon hands over; building it costs a few µs per burst in Python)."""
+        arr = bursts if isinstance(bursts, BurstArray) else BurstArray(bursts)
+        check(N.lib.infw_classify_bursts_host(self._ctx, dev, arr.arr, arr.n, chunk), "classify_bursts_host")
 
     def events_capture(self, frames, linear_len, ifindex, n_frames: int, events, events_count, samples,
                        pkt_len=None, offsets=None, stride: int = 0, dev: int = 0, stream=None) -> None:
@@ -506,6 +505,17 @@ class Burst:
         ptr = lambda a: None if a is None or a.size == 0 else a.ctypes.data  # noqa: E731
         return N.FrameBurst(ptr(self.frames), ptr(self.linear_len), ptr(self.pkt_len), self.n, self.ifindex, 0,
                             ptr(self.results), ptr(self.verdicts))
+
+
+class BurstArray:
+    """The struct infw_frame_burst array of a list of Burst, built once (keeps the bursts alive)."""
+
+    def __init__(self, bursts):
+        self.bursts = list(bursts)
+        self.n = len(self.bursts)
+        self.arr = (N.FrameBurst * max(1, self.n))()
+        for i, b in enumerate(self.bursts):
+            self.arr[i] = b.c()
 
 
 def pack_burst_host(burst: Burst) -> Dict[str, np.ndarray]:

@@ -311,3 +311,44 @@ def test_bursts_host_match_oracle(setup, chunk):
     for b, r, v in zip(bursts, want_r, want_v):
         assert np.array_equal(b.results, r) and np.array_equal(b.verdicts, v)
     assert np.array_equal(clf.stats_read_all(), wst)
+
+
+@pytest.mark.parametrize("arrays", ["own", "slices"])
+def test_small_bursts_host_match_oracle(setup, arrays):
+    """rx_burst-sized bursts (1..40 frames, ports interleaved) through infw_classify_bursts_host: thousands of segments
+    per chunk.  "own": every burst its own result / verdict arrays — a chunk's words come back in one copy and are
+    scattered on the host (abi.cpp xdp_scatter); "slices": the bursts' arrays are consecutive slices of one array per
+    call — adjacent destinations merge into one copy (xdp_copies).  Both: the oracle's words, verdicts and counters."""
+    from test_hostpack_cpu import _burst_of
+    wl, clf, m = setup
+    n = 30000
+    hdr, cap, pl, ifx = wl.frames(900000 + (arrays == "own") * n, n)
+    rng = np.random.default_rng(5)
+    cap = np.minimum(cap, rng.choice(np.array([60, 64, 128, 9000], np.uint32), n, p=[.3, .3, .2, .2])).astype(np.uint32)
+    buf, whole, _ = _burst_of(hdr, cap, pl, 0)
+    want_r, want_v, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    res = np.full(n, 0xFFFFFFFF, np.uint32)
+    ver = np.full(n, 7, np.uint8)
+    bursts, at = [], 0
+    while at < n:  # a burst holds frames of one port: cut where the port changes or at its size
+        size = int(rng.integers(1, 41))
+        hi = at + 1
+        while hi < min(n, at + size) and ifx[hi] == ifx[at]:
+            hi += 1
+        r = res[at:hi] if arrays == "slices" else np.full(hi - at, 0xFFFFFFFF, np.uint32)
+        v = ver[at:hi] if arrays == "slices" else np.full(hi - at, 7, np.uint8)
+        bursts.append((at, hi, infw.Burst(whole.frames[at:hi], cap[at:hi], pl[at:hi], int(ifx[at]), results=r,
+                                          verdicts=v)))
+        at = hi
+    assert len(bursts) > 2000
+    arr = infw.BurstArray([b for _, _, b in bursts])
+    for chunk in (4096, 0):
+        clf.stats_reset()
+        clf.classify_bursts_host(arr, chunk=chunk)
+        for lo, hi, b in bursts:
+            assert np.array_equal(b.results, want_r[lo:hi]) and np.array_equal(b.verdicts, want_v[lo:hi]), (chunk, lo)
+        assert np.array_equal(clf.stats_read_all(), wst)
+        for _, _, b in bursts:
+            b.results[:] = 0xFFFFFFFF
+            b.verdicts[:] = 7
+    del buf

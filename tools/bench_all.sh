@@ -30,6 +30,9 @@ run cfg2_xdp_registered --xdp-ring registered --no-cpu-baseline --steps 10 --war
 # the host-fed path: umem and rings in pageable memory, packed by the library's host threads (infw_classify_xdp_host)
 run cfg2_xdp_host_packed --xdp-ring host-packed --no-cpu-baseline --steps 10 --warmup 2
 run cfg2_xdp_host_packed_interleaved --xdp-ring host-packed --umem-order packet --no-cpu-baseline --steps 10 --warmup 2
+# the same frames as DPDK-style bursts (a pointer, data_len and pkt_len per frame: infw_classify_bursts_host)
+run cfg2_host_bursts --xdp-ring host-bursts --no-cpu-baseline --steps 10 --warmup 2
+run cfg2_host_bursts32 --xdp-ring host-bursts --burst-size 32 --no-cpu-baseline --steps 10 --warmup 2
 run cfg3_n1 --global-packets 1073741824 --no-cpu-baseline --steps 10 --warmup 2
 # the library's one-process shape: one context over N device slots (all on this GPU), a thread + stream per slot
 run inproc_n1 --in-process --gpus 1 --slots-on-gpu0 --global-packets 1073741824 --steps 5 --warmup 1 --no-line-rates

@@ -33,6 +33,8 @@ args_of() {  # bench.py arguments of a workload key
     cfg2w)  echo "--key-order workload" ;;
     xdphbm) echo "--xdp-ring hbm" ;;
     xdphp)  echo "--xdp-ring host-packed --steps 10 --warmup 2" ;;
+    xdphb)  echo "--xdp-ring host-bursts --steps 10 --warmup 2" ;;
+    xdphb32) echo "--xdp-ring host-bursts --burst-size 32 --steps 10 --warmup 2" ;;
     fused80)  echo "--from-frames 80 --fused" ;;
     fused256) echo "--from-frames 256 --fused" ;;
     fused512) echo "--from-frames 512 --fused" ;;

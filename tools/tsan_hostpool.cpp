@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -47,11 +48,18 @@ void check_chunk(const infw::XdpChunk &c, const std::vector<infw::XdpSeg> &segs)
                 flush();
                 group = p / INFW_V6_GROUP;
             }
-            const infw_xdp_desc &d = g.descs[i];
             infw_tuple t;
-            infw_pack_header(infw_xdp_frame(g.umem, d.addr), d.len, d.len, g.ifindex, &t);
+            uint32_t plen;
+            if (g.frames) {  // a burst: frame pointer, linear length, frame length
+                plen = g.pkt_len ? g.pkt_len[i] : g.linear_len[i];
+                infw_pack_header(g.frames[i], g.linear_len[i], plen, g.ifindex, &t);
+            } else {
+                const infw_xdp_desc &d = g.descs[i];
+                plen = d.len;
+                infw_pack_header(infw_xdp_frame(g.umem, d.addr), d.len, d.len, g.ifindex, &t);
+            }
             CHECK(c.out.saddr4[p] == t.saddr[0] && c.out.meta[p] == t.meta && c.out.l4word[p] == t.l4word &&
-                  c.out.pkt_len[p] == d.len);
+                  c.out.pkt_len[p] == plen);
             if (c.mixed) CHECK(c.out.ifindex[p] == g.ifindex);
             if ((t.meta & 0xFFFFu) == 0x86DDu) tails.insert(tails.end(), {t.saddr[1], t.saddr[2], t.saddr[3]});
         }
@@ -86,24 +94,60 @@ int main() {
         }
         rings.push_back(std::move(d));
     }
+    // DPDK-style bursts (infw_classify_bursts_host): 1..40 frames each, one of four ports, a pointer, linear length and
+    // frame length per frame (linear < frame length on some: a multi-segment mbuf) — thousands of segments per chunk
+    struct BurstArrays {
+        std::vector<const uint8_t *> frames;
+        std::vector<uint32_t> lin, plen;
+        uint32_t ifindex;
+    };
+    std::vector<BurstArrays> bursts;
+    for (uint64_t total = 0; total < 24000;) {
+        BurstArrays b;
+        const uint64_t n = 1 + g() % 40;
+        for (uint64_t i = 0; i < n; i++) {
+            b.frames.push_back(umem.data() + (g() % F) * kStride + (g() % 4 == 0 ? g() % 512 : 0));
+            const uint32_t pl = g() % 100 == 0 ? (uint32_t)(g() % 58) : 60 + (uint32_t)(g() % 9000);
+            b.plen.push_back(pl);
+            b.lin.push_back(g() % 3 == 0 ? std::min<uint32_t>(pl, (uint32_t)(g() % 80)) : std::min<uint32_t>(pl, 1500));
+        }
+        b.ifindex = 20 + (uint32_t)(g() % 4);
+        total += n;
+        bursts.push_back(std::move(b));
+    }
     uint64_t jobs = 0, chunks_checked = 0, mixed = 0;
     for (int threads : {1, 2, 3, 8}) {
         infw::HostPackPool pool(threads);
         for (uint64_t C : {512ull, 4096ull, 8192ull + 512}) {
-            for (int abort_at : {-1, 3}) {
-                // the rings cut as infw_classify_xdp_host cuts them: chunks of C running on from ring to ring
+            for (int abort_at : {-1, 3, -2}) {  // -2: the bursts, not aborted
+                // the rings (or bursts) cut as classify_host_fed cuts them: chunks of C running on from one to the next
                 std::vector<infw::XdpSeg> segs;
                 std::vector<infw::XdpChunk> chunks;
-                for (size_t r = 0; r < rings.size(); r++)
-                    for (uint64_t a = 0; a < rings[r].size();) {
+                auto add = [&](uint64_t n, uint32_t ifindex, auto &&seg_at) {
+                    for (uint64_t a = 0; a < n;) {
                         if (chunks.empty() || chunks.back().n == C)
                             chunks.push_back({(uint32_t)segs.size(), (uint32_t)segs.size(), 0, false, {}});
                         infw::XdpChunk &c = chunks.back();
-                        const uint64_t take = std::min(C - c.n, rings[r].size() - a);
-                        c.mixed |= c.seg1 > c.seg0 && segs[c.seg0].ifindex != 10 + r;
-                        segs.push_back({umem.data(), rings[r].data() + a, take, c.n, (uint32_t)(10 + r)});
+                        const uint64_t take = std::min(C - c.n, n - a);
+                        c.mixed |= c.seg1 > c.seg0 && segs[c.seg0].ifindex != ifindex;
+                        infw::XdpSeg sg = seg_at(a);
+                        sg.n = take, sg.pos = c.n, sg.ifindex = ifindex;
+                        segs.push_back(sg);
                         c.seg1++, c.n += take, a += take;
                     }
+                };
+                if (abort_at == -2) {
+                    for (const BurstArrays &b : bursts)
+                        add(b.frames.size(), b.ifindex, [&](uint64_t a) {
+                            infw::XdpSeg sg{nullptr, nullptr, 0, 0, 0};
+                            sg.frames = b.frames.data() + a, sg.linear_len = b.lin.data() + a, sg.pkt_len = b.plen.data() + a;
+                            return sg;
+                        });
+                } else {
+                    for (size_t r = 0; r < rings.size(); r++)
+                        add(rings[r].size(), (uint32_t)(10 + r),
+                            [&](uint64_t a) { return infw::XdpSeg{umem.data(), rings[r].data() + a, 0, 0, 0}; });
+                }
                 std::vector<std::vector<uint8_t>> slots(kSlots, std::vector<uint8_t>(32 * C));
                 for (size_t k = 0; k < chunks.size(); k++) {  // the slot layout of abi.cpp, stride S
                     const uint64_t S = (chunks[k].n + 63) & ~63ull;
@@ -147,7 +191,8 @@ int main() {
             }
         }
     }
-    printf("tsan_hostpool OK: %llu jobs, %llu chunks (%llu of several interfaces) checked against infw_pack_header\n",
-           (unsigned long long)jobs, (unsigned long long)chunks_checked, (unsigned long long)mixed);
+    printf("tsan_hostpool OK: %llu jobs, %llu chunks (%llu of several interfaces; rings and %zu bursts) checked against "
+           "infw_pack_header\n",
+           (unsigned long long)jobs, (unsigned long long)chunks_checked, (unsigned long long)mixed, bursts.size());
     return 0;
 }
