@@ -55,7 +55,13 @@ struct infw_frame_burst {
 /* read as 0, as kernel.c's data_end checks make them) and the packed tuples  */
 /* are pipelined through the device exactly as for AF_XDP rings (same chunks, */
 /* same options, same results as infw_classify_frames on the same frames).    */
-/* Synchronous; the whole call reads one table epoch.                         */
+/* Synchronous; the whole call reads one table epoch.  Hand many bursts to    */
+/* one call (every port's rx bursts of a poll round): the call passes over    */
+/* the array once and copies none of it; result arrays that continue one      */
+/* another (slices of one array) come back in one copy per run, arrays of     */
+/* their own are staged per chunk and scattered by the calling thread.        */
+/* -EINVAL for a burst with flags set or a null frames / linear_len array     */
+/* (nothing classified), -ENODEV for a host-only context.                     */
 int infw_classify_bursts_host(infw_ctx *ctx, int dev, const struct infw_frame_burst *bursts, uint32_t n_bursts,
                               uint64_t chunk);
 /* The burst packer alone on the calling thread (family-compact streams, as   */

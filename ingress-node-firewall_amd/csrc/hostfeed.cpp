@@ -59,10 +59,10 @@ HostPackPool::~HostPackPool() {
     for (auto &w : workers_) w.join();
 }
 
-void HostPackPool::begin(const std::vector<XdpChunk> *chunks, const std::vector<XdpSeg> *segs, uint64_t released) {
+void HostPackPool::begin(const std::vector<XdpChunk> *chunks, const HostFedSrc *src, uint64_t released) {
     // closed_ is set: no worker reads the fields below while they are written
     chunks_ = chunks;
-    segs_ = segs;
+    src_ = src;
     const size_t K = chunks->size();
     unit_base_.assign(K + 1, 0);
     for (size_t k = 0; k < K; k++)
@@ -96,7 +96,7 @@ void HostPackPool::end(bool abort) {
     }
     base_ += chunks_->size();
     chunks_ = nullptr;
-    segs_ = nullptr;
+    src_ = nullptr;
 }
 
 void HostPackPool::advance_frontier() {
@@ -111,7 +111,7 @@ void HostPackPool::advance_frontier() {
 void HostPackPool::pack_unit(uint64_t u, uint64_t k) {
     const XdpChunk &c = (*chunks_)[k];
     const uint64_t a = std::min(c.n, (u - unit_base_[k]) * kPackUnit), b = std::min(c.n, a + kPackUnit);
-    if (a < b && !abort_.load(std::memory_order_relaxed)) pack_chunk_range(c, *segs_, a, b);
+    if (a < b && !abort_.load(std::memory_order_relaxed)) pack_chunk_range(c, *src_, a, b);
 }
 
 bool HostPackPool::claim_and_pack(bool coordinator) {
@@ -215,43 +215,119 @@ void hostpack_burst(const uint8_t *const *frames, const uint32_t *linear_len, co
     }
 }
 
-void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64_t a, uint64_t b) {
+uint32_t HostFedSrc::at(uint64_t pos) const {
+    return (uint32_t)(std::upper_bound(start, start + count + 1, pos) - start) - 1;
+}
+
+// The chunk's next copy: merged into its last one when the destinations continue one another; past kXdpMaxCopies
+// the chunk is staged and keeps none.
+static void add_copy(XdpChunk &c, std::vector<XdpCopy> &v, uint32_t first, uint32_t &end, uint64_t pos, uint64_t n,
+                     uint8_t *dst, uint64_t bytes, uint32_t other) {
+    if (c.staged) return;
+    if (end > first && v[end - 1].pos + v[end - 1].n == pos && v[end - 1].dst + bytes * v[end - 1].n == dst) {
+        v[end - 1].n += n;
+        return;
+    }
+    if (end - first + other >= kXdpMaxCopies) {
+        c.staged = true;
+        return;
+    }
+    v.push_back({pos, n, dst});
+    end++;
+}
+
+int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t ce,
+               std::vector<uint64_t> &start, std::vector<XdpChunk> &chunks, std::vector<XdpCopy> &rcopies,
+               std::vector<XdpCopy> &vcopies, HostFedSrc &src) {
+    start.resize((size_t)count + 1);
+    chunks.clear(), rcopies.clear(), vcopies.clear();
+    src = HostFedSrc{rings, bursts, start.data(), count};
+    uint64_t pos = 0;
+    uint32_t first_if = 0;  // the current chunk's first ifindex
+    for (uint32_t i = 0; i < count; i++) {
+        uint64_t n;
+        uint32_t ifx;
+        uint32_t *res;
+        uint8_t *ver;
+        if (rings) {
+            const infw_xdp_ring &g = rings[i];
+            if (g.flags || (g.n && (!g.umem || !g.descs))) return -EINVAL;
+            n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
+        } else {
+            const infw_frame_burst &g = bursts[i];
+            if (g.flags || (g.n && (!g.frames || !g.linear_len))) return -EINVAL;
+            n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
+        }
+        start[i] = pos;
+        for (uint64_t a = 0; a < n;) {  // the chunks this source's frames fall in (one, for a small burst)
+            if (chunks.empty() || chunks.back().n == ce) {
+                if (!chunks.empty() && chunks.back().staged) {  // (a staged chunk keeps no copies)
+                    rcopies.resize(chunks.back().r0), vcopies.resize(chunks.back().v0);
+                    chunks.back().r1 = chunks.back().r0, chunks.back().v1 = chunks.back().v0;
+                }
+                const uint32_t r = (uint32_t)rcopies.size(), v = (uint32_t)vcopies.size();
+                chunks.push_back({pos + a, 0, i, i + 1, false, false, false, false, r, r, v, v, {}});
+                first_if = ifx;
+            }
+            XdpChunk &c = chunks.back();
+            const uint64_t take = std::min(ce - c.n, n - a);
+            c.mixed |= ifx != first_if;
+            c.src1 = i + 1;
+            if (res) {
+                c.any_res = true;
+                add_copy(c, rcopies, c.r0, c.r1, c.n, take, reinterpret_cast<uint8_t *>(res + a), 4, c.v1 - c.v0);
+            }
+            if (ver) {
+                c.any_ver = true;
+                add_copy(c, vcopies, c.v0, c.v1, c.n, take, ver + a, 1, c.r1 - c.r0);
+            }
+            c.n += take, a += take;
+        }
+        pos += n;
+    }
+    if (!chunks.empty() && chunks.back().staged) {
+        rcopies.resize(chunks.back().r0), vcopies.resize(chunks.back().v0);
+        chunks.back().r1 = chunks.back().r0, chunks.back().v1 = chunks.back().v0;
+    }
+    start[count] = pos;
+    return 0;
+}
+
+void pack_chunk_range(const XdpChunk &c, const HostFedSrc &src, uint64_t a, uint64_t b) {
     constexpr uint64_t G = INFW_V6_GROUP;
-    // the segment holding descriptor a (positions ascend within a chunk; a chunk of bursts may hold thousands)
-    uint32_t first = c.seg0;
-    if (c.seg1 - c.seg0 > 8)
-        first = (uint32_t)(std::upper_bound(segs.begin() + c.seg0, segs.begin() + c.seg1, a,
-                                            [](uint64_t v, const XdpSeg &g) { return v < g.pos; }) -
-                           segs.begin()) - 1;
-    for (uint32_t si = first; si < c.seg1 && segs[si].pos < b; si++) {
-        const XdpSeg &s = segs[si];
-        const uint64_t s0 = std::max(a, s.pos), s1 = std::min(b, s.pos + s.n);
-        for (uint64_t p = s0; p < s1;) {
+    const uint64_t A = c.begin + a, B = c.begin + b;  // call positions
+    for (uint32_t i = src.at(A); i < src.count && src.start[i] < B; i++) {
+        const uint64_t s0 = std::max(A, src.start[i]), s1 = std::min(B, src.start[i + 1]);
+        if (s0 >= s1) continue;  // (an empty source)
+        const uint32_t ifx = src.ifindex(i);
+        const infw_frame_burst *bu = src.bursts ? &src.bursts[i] : nullptr;
+        if (bu && i + 1 < src.count && s1 == src.start[i + 1]) {
+            // a burst's first frames are not prefetched by its own loop (which runs 16 frames ahead of itself): issue
+            // the next burst's while this one packs, so rx_burst-sized bursts keep as many misses in flight
+            const infw_frame_burst &nx = src.bursts[i + 1];
+            for (uint64_t q = 0, m = std::min<uint64_t>(nx.n, 16); q < m; q++) {
+                __builtin_prefetch(nx.frames[q] + 10);
+                __builtin_prefetch(nx.frames[q] + 57);
+            }
+        }
+        for (uint64_t p = s0 - c.begin, e1 = s1 - c.begin; p < e1;) {  // chunk positions
             const uint64_t g0 = p & ~(G - 1);
-            uint32_t rank = 0;  // IPv6 packets an earlier segment put into this group: they hold its first tail slots
-            uint64_t e = s1;
+            uint32_t rank = 0;  // IPv6 packets an earlier source put into this group: they hold its first tail slots
+            uint64_t e = e1;
             if (p != g0) {  // (the same thread packed them: units start on group boundaries)
                 for (uint64_t q = g0; q < p; q++) rank += (c.out.meta[q] & 0xFFFFu) == 0x86DDu;
-                e = std::min(s1, g0 + G);  // up to the group's end, so the packer's group boundaries stay aligned
+                e = std::min(e1, g0 + G);  // up to the group's end, so the packer's group boundaries stay aligned
             }
             const infw_hostpack_out o{c.out.saddr4 + p, c.out.v6tail + g0 / G * (12 * G) + 12 * rank,
                                       c.mixed ? c.out.ifindex + p : nullptr, c.out.pkt_len + p, c.out.meta + p,
                                       c.out.l4word + p};
-            if (s.frames && p == s0 && si + 1 < c.seg1 && segs[si + 1].frames) {
-                // a burst's first frames are not prefetched by its own loop (which runs 16 frames ahead of itself):
-                // issue them while this segment packs, so rx_burst-sized bursts keep as many misses in flight
-                const XdpSeg &nx = segs[si + 1];
-                for (uint64_t q = 0, m = std::min<uint64_t>(nx.n, 16); q < m; q++) {
-                    __builtin_prefetch(nx.frames[q] + 10);
-                    __builtin_prefetch(nx.frames[q] + 57);
-                }
-            }
-            if (s.frames)
-                hostpack_burst(s.frames + (p - s.pos), s.linear_len + (p - s.pos),
-                               s.pkt_len ? s.pkt_len + (p - s.pos) : nullptr, e - p, s.ifindex, o);
+            const uint64_t off = c.begin + p - src.start[i];  // the source's frame / descriptor index
+            if (bu)
+                hostpack_burst(bu->frames + off, bu->linear_len + off, bu->pkt_len ? bu->pkt_len + off : nullptr, e - p,
+                               ifx, o);
             else
-                infw_hostpack_xdp<INFW_PACK_PF, INFW_PACK_NT != 0>(s.umem, s.descs + (p - s.pos), e - p, s.ifindex,
-                                                                   o);
+                infw_hostpack_xdp<INFW_PACK_PF, INFW_PACK_NT != 0>(src.rings[i].umem, src.rings[i].descs + off, e - p,
+                                                                   ifx, o);
             p = e;
         }
     }

@@ -1,7 +1,7 @@
 // infw_hostfeed.h — the host packer threads of infw_classify_xdp_host (include/infw.h).
 //
-// A call's AF_XDP rings are cut into chunks of at most `chunk` descriptors that run on from one ring into the next (a
-// chunk holds one or more ring segments, back to back), and a pool of worker threads packs the chunks into a ring of
+// A call's AF_XDP rings (or bursts) are cut into chunks of at most `chunk` descriptors that run on from one ring into
+// the next (a chunk holds the tail of one, whole ones, the head of another, back to back), and a pool of worker threads packs the chunks into a ring of
 // pinned host slots, in chunk order, while the calling thread — the coordinator — moves packed chunks through the
 // device (H2D, classify, D2H) and packs too whenever it would otherwise wait.  Work is handed out dynamically: every
 // chunk is cut into units of kPackUnit descriptors (whole INFW_V6_GROUP groups), numbered across the call, and a
@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/infw.h"
+#include "../../include/infw_host.h"
 #include "infw_hostpack.h"
 
 namespace infw {
@@ -41,30 +42,53 @@ class Signal {
     std::condition_variable cv_;
 };
 
-// One ring's run of descriptors inside a chunk, at chunk positions [pos, pos + n): an AF_XDP ring's (umem +
-// descriptors) or a burst's (frame pointers + linear and frame lengths; frames != nullptr).
-struct XdpSeg {
-    const uint8_t *umem;
-    const infw_xdp_desc *descs;
-    uint64_t n, pos;
-    uint32_t ifindex;
-    const uint8_t *const *frames = nullptr;
-    const uint32_t *linear_len = nullptr, *pkt_len = nullptr;
+// A call's sources as the caller handed them over — AF_XDP rings (umem + descriptors) or DPDK-style bursts (frame
+// pointers + linear and frame lengths): exactly one of `rings` / `bursts` is set — laid end to end at call positions:
+// source i holds positions [start[i], start[i + 1]).  No per-source copy is made: a call of half a million
+// rx_burst-sized bursts costs one pass that writes 8 B per burst.
+struct HostFedSrc {
+    const infw_xdp_ring *rings = nullptr;
+    const infw_frame_burst *bursts = nullptr;
+    const uint64_t *start = nullptr;  // count + 1 entries
+    uint32_t count = 0;
+    uint32_t ifindex(uint32_t i) const { return rings ? rings[i].ifindex : bursts[i].ifindex; }
+    uint32_t *results(uint32_t i) const { return rings ? rings[i].results : bursts[i].results; }
+    uint8_t *verdicts(uint32_t i) const { return rings ? rings[i].verdicts : bursts[i].verdicts; }
+    // the source holding call position pos < start[count] (empty sources share their start with the next one)
+    uint32_t at(uint64_t pos) const;
 };
 
 // A burst's frames [0, n) -> the family-compact streams (host code; the burst form of infw_hostpack_xdp).
 void hostpack_burst(const uint8_t *const *frames, const uint32_t *linear_len, const uint32_t *pkt_len, uint64_t n,
                     uint32_t ifindex, const infw_hostpack_out &o);
 
-// A chunk: segments [seg0, seg1) of the call's segment list, n descriptors in all.  `mixed`: its segments carry more
-// than one ifindex, so the packers write the ifindex stream (else the device fills it).  `out`: the chunk's streams in
-// its host slot (positions 0..n-1).
+// One D2H copy of a chunk's result words or verdicts: chunk positions [pos, pos + n) to dst.
+struct XdpCopy {
+    uint64_t pos, n;
+    uint8_t *dst;
+};
+constexpr uint32_t kXdpMaxCopies = 16;  // copies per chunk before its words are staged and scattered on the host
+
+// A chunk: call positions [begin, begin + n), sources [src0, src1).  `mixed`: its sources carry more than one
+// ifindex, so the packers write the ifindex stream (else the device fills it).  Its D2H copies: result words
+// rcopies[r0, r1), verdicts vcopies[v0, v1) — sources whose arrays continue one another merge into one copy — or,
+// `staged`, more than kXdpMaxCopies of them: the chunk comes back in one copy of each kind, scattered on the host.
+// `out`: the chunk's streams in its host slot (positions 0..n-1).
 struct XdpChunk {
-    uint32_t seg0, seg1;
-    uint64_t n;
-    bool mixed;
+    uint64_t begin, n;
+    uint32_t src0, src1;
+    bool mixed, staged, any_res, any_ver;
+    uint32_t r0, r1, v0, v1;
     infw_hostpack_out out;
 };
+
+// The sources cut into chunks of at most ce positions (ce a multiple of INFW_V6_GROUP), running on from one source
+// into the next, in one pass over the caller's array: fills start (count + 1 entries), chunks (their `out` left for
+// the caller) and their D2H copies.  -EINVAL for a source with flags set or a null array it needs (nothing is packed
+// then).
+int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t ce,
+               std::vector<uint64_t> &start, std::vector<XdpChunk> &chunks, std::vector<XdpCopy> &rcopies,
+               std::vector<XdpCopy> &vcopies, HostFedSrc &src);
 
 constexpr uint64_t kPackUnit = 4096;  // descriptors per claimed unit (~30 us of one core's packing)
 
@@ -73,9 +97,9 @@ class HostPackPool {
     explicit HostPackPool(int threads);
     ~HostPackPool();
     int threads() const { return n_threads_; }
-    // Start packing `chunks` (segments in `segs`; at most `released` chunks before release() allows more).  Both
-    // vectors must outlive end().
-    void begin(const std::vector<XdpChunk> *chunks, const std::vector<XdpSeg> *segs, uint64_t released);
+    // Start packing `chunks` of `src` (at most `released` chunks before release() allows more).  Both must outlive
+    // end().
+    void begin(const std::vector<XdpChunk> *chunks, const HostFedSrc *src, uint64_t released);
     // The coordinator's wait for chunk k: it packs released units itself until k is packed.
     void help_until_packed(uint64_t k);
     void release(uint64_t upto) { released_.set(base_ + upto); }  // chunks < upto may be packed
@@ -103,7 +127,7 @@ class HostPackPool {
     std::mutex frontier_mu_;
     uint64_t frontier_ = 0;  // chunks < frontier_ are packed (under frontier_mu_)
     const std::vector<XdpChunk> *chunks_ = nullptr;
-    const std::vector<XdpSeg> *segs_ = nullptr;
+    const HostFedSrc *src_ = nullptr;
     uint64_t base_ = 0;  // chunk sequence number of the job's chunk 0 (the signals only grow)
     uint64_t gen_ = 0;
     std::atomic<bool> abort_{false}, quit_{false};
@@ -111,8 +135,8 @@ class HostPackPool {
     int n_threads_;
 };
 
-// Pack chunk positions [a, b) of `c` (a on an INFW_V6_GROUP boundary) from its segments into c.out.
-void pack_chunk_range(const XdpChunk &c, const std::vector<XdpSeg> &segs, uint64_t a, uint64_t b);
+// Pack chunk positions [a, b) of `c` (a on an INFW_V6_GROUP boundary) from its sources into c.out.
+void pack_chunk_range(const XdpChunk &c, const HostFedSrc &src, uint64_t a, uint64_t b);
 
 // Worker threads for a pool: option host_threads, or (0) the CPUs this process may run on — its affinity mask, capped
 // by a cgroup v2 CPU quota (cpu.max) — at most 16.

@@ -33,34 +33,36 @@ constexpr int kSlots = 3;
 
 // The chunk's streams against infw_pack_header (infw_pack.h: what kernel.c reads) on every descriptor, position by
 // position; the v6tail blocks hold each group's IPv6 packets' address bytes 4..15 in position order.
-void check_chunk(const infw::XdpChunk &c, const std::vector<infw::XdpSeg> &segs) {
+void check_chunk(const infw::XdpChunk &c, const infw::HostFedSrc &src) {
     std::vector<uint32_t> tails;
     uint64_t group = 0;
     auto flush = [&]() {
         CHECK(memcmp(c.out.v6tail + group * 12 * INFW_V6_GROUP, tails.data(), 4 * tails.size()) == 0);
         tails.clear();
     };
-    for (uint32_t si = c.seg0; si < c.seg1; si++) {
-        const infw::XdpSeg &g = segs[si];
-        for (uint64_t i = 0; i < g.n; i++) {
-            const uint64_t p = g.pos + i;
+    for (uint32_t si = c.src0; si < c.src1; si++) {
+        const uint64_t s0 = std::max(c.begin, src.start[si]), s1 = std::min(c.begin + c.n, src.start[si + 1]);
+        for (uint64_t q = s0; q < s1; q++) {
+            const uint64_t p = q - c.begin, i = q - src.start[si];
             if (p / INFW_V6_GROUP != group) {
                 flush();
                 group = p / INFW_V6_GROUP;
             }
             infw_tuple t;
             uint32_t plen;
-            if (g.frames) {  // a burst: frame pointer, linear length, frame length
-                plen = g.pkt_len ? g.pkt_len[i] : g.linear_len[i];
-                infw_pack_header(g.frames[i], g.linear_len[i], plen, g.ifindex, &t);
+            if (src.bursts) {  // a burst: frame pointer, linear length, frame length
+                const infw_frame_burst &b = src.bursts[si];
+                plen = b.pkt_len ? b.pkt_len[i] : b.linear_len[i];
+                infw_pack_header(b.frames[i], b.linear_len[i], plen, b.ifindex, &t);
             } else {
-                const infw_xdp_desc &d = g.descs[i];
+                const infw_xdp_ring &r = src.rings[si];
+                const infw_xdp_desc &d = r.descs[i];
                 plen = d.len;
-                infw_pack_header(infw_xdp_frame(g.umem, d.addr), d.len, d.len, g.ifindex, &t);
+                infw_pack_header(infw_xdp_frame(r.umem, d.addr), d.len, d.len, r.ifindex, &t);
             }
             CHECK(c.out.saddr4[p] == t.saddr[0] && c.out.meta[p] == t.meta && c.out.l4word[p] == t.l4word &&
                   c.out.pkt_len[p] == plen);
-            if (c.mixed) CHECK(c.out.ifindex[p] == g.ifindex);
+            if (c.mixed) CHECK(c.out.ifindex[p] == src.ifindex(si));
             if ((t.meta & 0xFFFFu) == 0x86DDu) tails.insert(tails.end(), {t.saddr[1], t.saddr[2], t.saddr[3]});
         }
     }
@@ -83,7 +85,7 @@ int main() {
         h[12] = et >> 8, h[13] = et & 0xFF;
     }
     const uint64_t ring_sizes[] = {0, 1, 63, 4097, 20000, 35000 - 1};
-    std::vector<std::vector<infw_xdp_desc>> rings;
+    std::vector<std::vector<infw_xdp_desc>> rd;
     for (uint64_t sz : ring_sizes) {
         std::vector<infw_xdp_desc> d(sz);
         for (auto &x : d) {
@@ -92,8 +94,11 @@ int main() {
             x.len = g() % 100 == 0 ? (uint32_t)(g() % 58) : 60 + (uint32_t)(g() % 1400);
             x.options = 0;
         }
-        rings.push_back(std::move(d));
+        rd.push_back(std::move(d));
     }
+    std::vector<infw_xdp_ring> rings;  // ring r on interface 10 + r
+    for (size_t r = 0; r < rd.size(); r++)
+        rings.push_back({umem.data(), rd[r].data(), rd[r].size(), (uint32_t)(10 + r), 0, nullptr, nullptr});
     // DPDK-style bursts (infw_classify_bursts_host): 1..40 frames each, one of four ports, a pointer, linear length and
     // frame length per frame (linear < frame length on some: a multi-segment mbuf) — thousands of segments per chunk
     struct BurstArrays {
@@ -101,7 +106,7 @@ int main() {
         std::vector<uint32_t> lin, plen;
         uint32_t ifindex;
     };
-    std::vector<BurstArrays> bursts;
+    std::vector<BurstArrays> ba;
     for (uint64_t total = 0; total < 24000;) {
         BurstArrays b;
         const uint64_t n = 1 + g() % 40;
@@ -113,41 +118,24 @@ int main() {
         }
         b.ifindex = 20 + (uint32_t)(g() % 4);
         total += n;
-        bursts.push_back(std::move(b));
+        ba.push_back(std::move(b));
     }
+    std::vector<infw_frame_burst> bursts;
+    for (const BurstArrays &b : ba)
+        bursts.push_back({b.frames.data(), b.lin.data(), b.plen.data(), b.frames.size(), b.ifindex, 0, nullptr, nullptr});
     uint64_t jobs = 0, chunks_checked = 0, mixed = 0;
     for (int threads : {1, 2, 3, 8}) {
         infw::HostPackPool pool(threads);
         for (uint64_t C : {512ull, 4096ull, 8192ull + 512}) {
             for (int abort_at : {-1, 3, -2}) {  // -2: the bursts, not aborted
                 // the rings (or bursts) cut as classify_host_fed cuts them: chunks of C running on from one to the next
-                std::vector<infw::XdpSeg> segs;
+                std::vector<uint64_t> start;
                 std::vector<infw::XdpChunk> chunks;
-                auto add = [&](uint64_t n, uint32_t ifindex, auto &&seg_at) {
-                    for (uint64_t a = 0; a < n;) {
-                        if (chunks.empty() || chunks.back().n == C)
-                            chunks.push_back({(uint32_t)segs.size(), (uint32_t)segs.size(), 0, false, {}});
-                        infw::XdpChunk &c = chunks.back();
-                        const uint64_t take = std::min(C - c.n, n - a);
-                        c.mixed |= c.seg1 > c.seg0 && segs[c.seg0].ifindex != ifindex;
-                        infw::XdpSeg sg = seg_at(a);
-                        sg.n = take, sg.pos = c.n, sg.ifindex = ifindex;
-                        segs.push_back(sg);
-                        c.seg1++, c.n += take, a += take;
-                    }
-                };
-                if (abort_at == -2) {
-                    for (const BurstArrays &b : bursts)
-                        add(b.frames.size(), b.ifindex, [&](uint64_t a) {
-                            infw::XdpSeg sg{nullptr, nullptr, 0, 0, 0};
-                            sg.frames = b.frames.data() + a, sg.linear_len = b.lin.data() + a, sg.pkt_len = b.plen.data() + a;
-                            return sg;
-                        });
-                } else {
-                    for (size_t r = 0; r < rings.size(); r++)
-                        add(rings[r].size(), (uint32_t)(10 + r),
-                            [&](uint64_t a) { return infw::XdpSeg{umem.data(), rings[r].data() + a, 0, 0, 0}; });
-                }
+                std::vector<infw::XdpCopy> rc, vc;
+                infw::HostFedSrc src;
+                CHECK(abort_at == -2
+                          ? infw::cut_chunks(nullptr, bursts.data(), (uint32_t)bursts.size(), C, start, chunks, rc, vc, src) == 0
+                          : infw::cut_chunks(rings.data(), nullptr, (uint32_t)rings.size(), C, start, chunks, rc, vc, src) == 0);
                 std::vector<std::vector<uint8_t>> slots(kSlots, std::vector<uint8_t>(32 * C));
                 for (size_t k = 0; k < chunks.size(); k++) {  // the slot layout of abi.cpp, stride S
                     const uint64_t S = (chunks[k].n + 63) & ~63ull;
@@ -158,7 +146,7 @@ int main() {
                     mixed += chunks[k].mixed;
                 }
                 const uint64_t K = chunks.size();
-                pool.begin(&chunks, &segs, std::min<uint64_t>(K, kSlots));
+                pool.begin(&chunks, &src, std::min<uint64_t>(K, kSlots));
                 bool aborted = false;
                 for (uint64_t k = 0; k < K; k++) {
                     if ((int64_t)k == abort_at) {
@@ -166,7 +154,7 @@ int main() {
                         break;
                     }
                     pool.help_until_packed(k);  // the coordinator packs too
-                    check_chunk(chunks[k], segs);
+                    check_chunk(chunks[k], src);
                     chunks_checked++;
                     pool.release(k + kSlots + 1);  // slot k % 3 is free again: chunk k + 3 may fill it
                 }
@@ -175,16 +163,20 @@ int main() {
                 // small calls right behind it, while workers may still be waking for the last job: one chunk of a
                 // 1-descriptor and a 63-descriptor ring (one unit, no worker woken), packed by the coordinator
                 for (int rep = 0; rep < 20; rep++) {
-                    std::vector<infw::XdpSeg> ss = {{umem.data(), rings[1].data(), 1, 0, 11},
-                                                    {umem.data(), rings[2].data(), 63, 1, 12}};
-                    std::vector<infw::XdpChunk> cc = {{0, 2, 64, true, {}}};
+                    const infw_xdp_ring small[2] = {{umem.data(), rd[1].data(), 1, 11, 0, nullptr, nullptr},
+                                                    {umem.data(), rd[2].data(), 63, 12, 0, nullptr, nullptr}};
+                    std::vector<uint64_t> ss;
+                    std::vector<infw::XdpChunk> cc;
+                    std::vector<infw::XdpCopy> rc, vc;
+                    infw::HostFedSrc sm;
+                    CHECK(infw::cut_chunks(small, nullptr, 2, 512, ss, cc, rc, vc, sm) == 0 && cc.size() == 1 && cc[0].mixed);
                     uint8_t *b = slots[0].data();
                     cc[0].out = {reinterpret_cast<uint32_t *>(b), b + 16 * 64, reinterpret_cast<uint32_t *>(b + 28 * 64),
                                  reinterpret_cast<uint32_t *>(b + 4 * 64), reinterpret_cast<uint32_t *>(b + 8 * 64),
                                  reinterpret_cast<uint32_t *>(b + 12 * 64)};
-                    pool.begin(&cc, &ss, 1);
+                    pool.begin(&cc, &sm, 1);
                     pool.help_until_packed(0);
-                    check_chunk(cc[0], ss);
+                    check_chunk(cc[0], sm);
                     pool.end(false);
                     jobs++, chunks_checked++, mixed++;
                 }
