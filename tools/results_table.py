@@ -23,7 +23,7 @@ PROF = {  # bench_all.sh line -> gpu_pass.sh profile key
 ORDER = ["cfg2", "cfg2_compact", "cfg1", "cfg1_compact", "cfg4", "cfg4_1m", "cfg2_uniform", "cfg2_distinct",
          "cfg2_distinct_popularity_order", "cfg3_n1", "inproc_n1", "inproc_n8", "cfg2_frames", "cfg2_frames_fused",
          "cfg2_xdp_hbm", "cfg2_xdp_host", "cfg2_xdp_registered", "cfg2_xdp_host_packed",
-         "cfg2_xdp_host_packed_interleaved"]
+         "cfg2_xdp_host_packed_interleaved", "cfg2_host_bursts", "cfg2_host_bursts32"]
 LABEL = {
     "cfg2": "configs[2] (headline)", "cfg2_compact": "configs[2], family-compact", "cfg1": "configs[1]",
     "cfg1_compact": "configs[1], family-compact", "cfg4": "configs[4]", "cfg4_1m": "configs[4] at 1M prefixes",
@@ -36,6 +36,8 @@ LABEL = {
     "cfg2_xdp_registered": "AF_XDP rings, daemon's registered umem (device read)",
     "cfg2_xdp_host_packed": "AF_XDP rings, pageable umem, host-fed (ring order)",
     "cfg2_xdp_host_packed_interleaved": "the same, rings interleaved in one umem",
+    "cfg2_host_bursts": "DPDK-style bursts, host-fed (one burst per port)",
+    "cfg2_host_bursts32": "DPDK-style bursts of 32 frames, host-fed",
 }
 
 
