@@ -7,9 +7,9 @@ run's launches); roofline.frac (algorithmic bytes / HIP-event time / 8 TB/s); HB
 requests (TCC_EA0_RDREQ) x 128 B per second against the stream bandwidth the same line measured in its own process,
 and its inverse (the most the kernel could gain at today's lines per packet if every random line moved at the
 streaming rate).  Lines whose build id differs from the profile's are refused.
-Usage: tools/results_table.py <pass> [<override pass>]  (e.g. r06z r06w: lines present in profiles/<override>/lines
-replace the pass's own — a component re-measured after a host-side change at the same kernel build)
-  -> markdown on stdout, JSON in profiles/<pass>/results.json"""
+Usage: tools/results_table.py <pass> [<override pass>]  (e.g. r06z r06F: lines present in profiles/<override>/lines,
+and profiles <override>_<key>, replace the pass's own — re-measured after a host-side change at the same kernel build)
+  -> markdown on stdout, JSON in profiles/<override or pass>/results.json"""
 import json
 import os
 import sys
@@ -67,7 +67,12 @@ def main():
                "packets_per_launch": n, "kernel_ms_hip": k_ms, "frac": r.get("frac"), "bound": r.get("bound"),
                "algo_B": r.get("algorithmic_bytes_per_packet")}
         key = PROF.get(name)
-        sp = os.path.join(ROOT, "profiles", f"{tag}_{key}", "summary.json") if key else None
+        sp = None
+        for t in ([over] if over else []) + [tag]:  # the override pass's profile of the workload first
+            q = os.path.join(ROOT, "profiles", f"{t}_{key}", "summary.json") if key else None
+            if q and os.path.exists(q):
+                sp, ptag = q, t
+                break
         if sp and os.path.exists(sp):
             s = json.load(open(sp))
             bl = s.get("bench_line_under_kernel_trace", {})
@@ -76,13 +81,13 @@ def main():
             rings = (r.get("xdp_ring") or {}).get("rings") or 1  # AF_XDP: one launch per ring, the line's time per step
             row.update(rocprof_ms=s["avg_ns_per_classification"] * rings / 1e6, hbm_B=s["hbm_bytes_per_packet"],
                        hits=s["l2_hits_per_packet"], misses=s["l2_misses_per_packet"],
-                       fabric_req=s["ea_rdreq_per_packet"], profile=f"profiles/{tag}_{key}")
+                       fabric_req=s["ea_rdreq_per_packet"], profile=f"profiles/{ptag}_{key}")
             if stream and k_ms:  # per step: the step's packets over the step's kernel time (AF_XDP: one launch per ring)
                 tb = s["ea_rdreq_per_packet"] * 128 * n / (k_ms * 1e-3) / 1e9
                 row.update(line_TBps=tb / 1e3, line_frac=tb / stream, headroom=stream / tb)
         rows.append(row)
         out[name] = row
-    json.dump(out, open(os.path.join(ROOT, "profiles", tag, "results.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", over or tag, "results.json"), "w"), indent=1)
 
     def f(v, fmt):
         return format(v, fmt) if isinstance(v, (int, float)) else "—"
