@@ -6,7 +6,10 @@
 // start in one ring's segment and end in the next's), starts a job over three host slots, packs units itself until
 // chunk k is packed, checks the slot's streams against infw_pack_header on every descriptor, and then releases chunk
 // k + 3 into the slot it has just freed — for several thread counts and chunk sizes, jobs back to back on one pool
-// (small ones wake no worker), and a job aborted half-way (end(true): no worker may still touch the job after).
+// (small ones wake no worker), and a job aborted half-way (end(true): no worker may still touch the job after).  The
+// same for DPDK-style bursts of 1..40 frames (thousands of sources per chunk); and the D2H plan cut_chunks makes for
+// each chunk (copy runs, or staging past kXdpMaxCopies), played on the host for bursts whose arrays are slices of one
+// array, bursts with arrays of their own, and rings.
 // Prints "tsan_hostpool OK ..." and exits 0.
 #include <stdio.h>
 #include <stdlib.h>
@@ -69,6 +72,38 @@ void check_chunk(const infw::XdpChunk &c, const infw::HostFedSrc &src) {
     flush();
 }
 
+// The D2H plan cut_chunks made for a chunk, played on the host: device words = a function of the chunk position, moved
+// by the chunk's copies (or, staged, scattered source by source as abi.cpp xdp_scatter does), then every source's
+// result array and verdicts checked word by word.  Returns the copies the chunk needed (0 when staged).
+uint32_t check_copies(const infw::XdpChunk &c, const std::vector<infw::XdpCopy> &rc, const std::vector<infw::XdpCopy> &vc,
+                      const infw::HostFedSrc &src, uint32_t salt) {
+    std::vector<uint32_t> dres(c.n);
+    std::vector<uint8_t> dver(c.n);
+    for (uint64_t p = 0; p < c.n; p++) dres[p] = (uint32_t)p * 2654435761u ^ salt, dver[p] = (uint8_t)(p * 7 + salt);
+    if (c.staged) {
+        CHECK(c.r0 == c.r1 && c.v0 == c.v1);
+        for (uint32_t i = c.src0; i < c.src1; i++) {
+            const uint64_t s0 = std::max(c.begin, src.start[i]), s1 = std::min(c.begin + c.n, src.start[i + 1]);
+            if (s0 >= s1) continue;
+            if (uint32_t *r = src.results(i)) memcpy(r + (s0 - src.start[i]), dres.data() + (s0 - c.begin), 4 * (s1 - s0));
+            if (uint8_t *v = src.verdicts(i)) memcpy(v + (s0 - src.start[i]), dver.data() + (s0 - c.begin), s1 - s0);
+        }
+    } else {
+        CHECK(c.r1 - c.r0 + c.v1 - c.v0 <= infw::kXdpMaxCopies);
+        for (uint32_t i = c.r0; i < c.r1; i++) memcpy(rc[i].dst, dres.data() + rc[i].pos, 4 * rc[i].n);
+        for (uint32_t i = c.v0; i < c.v1; i++) memcpy(vc[i].dst, dver.data() + vc[i].pos, vc[i].n);
+    }
+    for (uint32_t i = c.src0; i < c.src1; i++) {
+        const uint64_t s0 = std::max(c.begin, src.start[i]), s1 = std::min(c.begin + c.n, src.start[i + 1]);
+        for (uint64_t q = s0; q < s1; q++) {
+            const uint64_t p = q - c.begin, j = q - src.start[i];
+            if (const uint32_t *r = src.results(i)) CHECK(r[j] == dres[p]);
+            if (const uint8_t *v = src.verdicts(i)) CHECK(v[j] == dver[p]);
+        }
+    }
+    return c.staged ? 0 : c.r1 - c.r0 + c.v1 - c.v0;
+}
+
 }  // namespace
 
 int main() {
@@ -123,6 +158,44 @@ int main() {
     std::vector<infw_frame_burst> bursts;
     for (const BurstArrays &b : ba)
         bursts.push_back({b.frames.data(), b.lin.data(), b.plen.data(), b.frames.size(), b.ifindex, 0, nullptr, nullptr});
+    // the D2H plans of bursts whose result words and verdicts are slices of one array per call (every chunk one copy
+    // of each kind, whatever its bursts) and of bursts with arrays of their own (chunks of many bursts staged), and of
+    // the rings (their own arrays)
+    uint64_t plans = 0, staged = 0;
+    {
+        uint64_t total = 0;
+        for (const BurstArrays &b : ba) total += b.frames.size();
+        std::vector<uint32_t> all_r(total), own_r(total);
+        std::vector<uint8_t> all_v(total), own_v(total);
+        std::vector<infw_frame_burst> sl = bursts, own = bursts;
+        for (size_t i = 0, at = 0; i < bursts.size(); at += bursts[i].n, i++) {
+            sl[i].results = all_r.data() + at, sl[i].verdicts = all_v.data() + at;
+            own[i].results = own_r.data() + at + 0, own[i].verdicts = nullptr;
+            if (i % 2) own[i].results = nullptr;  // (own arrays: every other burst wants no words; none adjacent)
+        }
+        std::vector<std::vector<uint32_t>> rr(rings.size());
+        std::vector<infw_xdp_ring> rg = rings;
+        for (size_t r = 0; r < rings.size(); r++) rr[r].resize(rings[r].n + 1), rg[r].results = rr[r].data();
+        for (uint64_t C : {512ull, 4096ull, 8192ull + 512}) {
+            std::vector<uint64_t> st;
+            std::vector<infw::XdpChunk> ch;
+            std::vector<infw::XdpCopy> rc, vc;
+            infw::HostFedSrc sv;
+            CHECK(infw::cut_chunks(nullptr, sl.data(), (uint32_t)sl.size(), C, st, ch, rc, vc, sv) == 0);
+            for (auto &c : ch) {
+                CHECK(!c.staged && c.r1 - c.r0 == 1 && c.v1 - c.v0 == 1);  // slices: one copy of each kind per chunk
+                check_copies(c, rc, vc, sv, (uint32_t)C), plans++;
+            }
+            CHECK(infw::cut_chunks(nullptr, own.data(), (uint32_t)own.size(), C, st, ch, rc, vc, sv) == 0);
+            for (auto &c : ch) check_copies(c, rc, vc, sv, (uint32_t)C + 1), plans++, staged += c.staged;
+            CHECK(infw::cut_chunks(rg.data(), nullptr, (uint32_t)rg.size(), C, st, ch, rc, vc, sv) == 0);
+            for (auto &c : ch) {
+                CHECK(!c.staged);
+                check_copies(c, rc, vc, sv, (uint32_t)C + 2), plans++;
+            }
+        }
+        CHECK(staged > 0);
+    }
     uint64_t jobs = 0, chunks_checked = 0, mixed = 0;
     for (int threads : {1, 2, 3, 8}) {
         infw::HostPackPool pool(threads);
@@ -184,7 +257,8 @@ int main() {
         }
     }
     printf("tsan_hostpool OK: %llu jobs, %llu chunks (%llu of several interfaces; rings and %zu bursts) checked against "
-           "infw_pack_header\n",
-           (unsigned long long)jobs, (unsigned long long)chunks_checked, (unsigned long long)mixed, bursts.size());
+           "infw_pack_header; %llu D2H plans (%llu staged) played and checked\n",
+           (unsigned long long)jobs, (unsigned long long)chunks_checked, (unsigned long long)mixed, bursts.size(),
+           (unsigned long long)plans, (unsigned long long)staged);
     return 0;
 }
