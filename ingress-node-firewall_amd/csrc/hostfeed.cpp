@@ -219,77 +219,166 @@ uint32_t HostFedSrc::at(uint64_t pos) const {
     return (uint32_t)(std::upper_bound(start, start + count + 1, pos) - start) - 1;
 }
 
-// The chunk's next copy: merged into its last one when the destinations continue one another; past kXdpMaxCopies
-// the chunk is staged and keeps none.
-static void add_copy(XdpChunk &c, std::vector<XdpCopy> &v, uint32_t first, uint32_t &end, uint64_t pos, uint64_t n,
-                     uint8_t *dst, uint64_t bytes, uint32_t other) {
-    if (c.staged) return;
-    if (end > first && v[end - 1].pos + v[end - 1].n == pos && v[end - 1].dst + bytes * v[end - 1].n == dst) {
-        v[end - 1].n += n;
+uint64_t chunk_positions(uint64_t total, uint64_t chunk, bool auto_chunk) {
+    if (auto_chunk && total < 4 * chunk)
+        return std::min(chunk, std::max<uint64_t>(32768, ((total + 3) / 4 + 4095) & ~4095ull));
+    return chunk;
+}
+
+namespace {
+
+// Source i's fields; false for a source with flags set or a null array it needs.
+inline bool source_fields(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t i, uint64_t &n,
+                          uint32_t &ifx, uint32_t *&res, uint8_t *&ver) {
+    if (rings) {
+        const infw_xdp_ring &g = rings[i];
+        n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
+        return !(g.flags || (g.n && (!g.umem || !g.descs)));
+    }
+    const infw_frame_burst &g = bursts[i];
+    n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
+    return !(g.flags || (g.n && (!g.frames || !g.linear_len)));
+}
+
+// A copy appended to a chunk's copies [first, end) of one kind: merged into the last one when the destinations
+// continue one another.
+inline void append_copy(std::vector<XdpCopy> &v, uint32_t first, uint32_t &end, const XdpCopy &q, uint64_t bytes) {
+    if (end > first && v[end - 1].pos + v[end - 1].n == q.pos && v[end - 1].dst + bytes * v[end - 1].n == q.dst) {
+        v[end - 1].n += q.n;
         return;
     }
-    if (end - first + other >= kXdpMaxCopies) {
-        c.staged = true;
-        return;
-    }
-    v.push_back({pos, n, dst});
+    v.push_back(q);
     end++;
 }
 
-int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t ce,
-               std::vector<uint64_t> &start, std::vector<XdpChunk> &chunks, std::vector<XdpCopy> &rcopies,
-               std::vector<XdpCopy> &vcopies, HostFedSrc &src) {
-    start.resize((size_t)count + 1);
-    chunks.clear(), rcopies.clear(), vcopies.clear();
-    src = HostFedSrc{rings, bursts, start.data(), count};
-    uint64_t pos = 0;
-    uint32_t first_if = 0;  // the current chunk's first ifindex
-    for (uint32_t i = 0; i < count; i++) {
-        uint64_t n;
-        uint32_t ifx;
-        uint32_t *res;
-        uint8_t *ver;
-        if (rings) {
-            const infw_xdp_ring &g = rings[i];
-            if (g.flags || (g.n && (!g.umem || !g.descs))) return -EINVAL;
-            n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
-        } else {
-            const infw_frame_burst &g = bursts[i];
-            if (g.flags || (g.n && (!g.frames || !g.linear_len))) return -EINVAL;
-            n = g.n, ifx = g.ifindex, res = g.results, ver = g.verdicts;
+// A staged chunk keeps no copies (they are the last ones of their vectors).
+inline void seal(XdpChunk &c, std::vector<XdpCopy> &rc, std::vector<XdpCopy> &vc) {
+    if (!c.staged) return;
+    rc.resize(c.r0), vc.resize(c.v0);
+    c.r1 = c.r0, c.v1 = c.v0;
+}
+
+// One thread's share of the sources [lo, hi): its pieces of chunks (a chunk's positions this share holds, its copies
+// in the share's own vectors), merged in order afterwards.
+struct CutPart {
+    uint32_t lo = 0, hi = 0;
+    uint64_t base = 0, sum = 0;
+    bool bad = false;
+    std::vector<XdpChunk> pieces;
+    std::vector<uint32_t> first_if;  // per piece: its first source's ifindex
+    std::vector<XdpCopy> rc, vc;
+};
+
+void part_count(CutPart &p, const infw_xdp_ring *rings, const infw_frame_burst *bursts) {
+    uint64_t n;
+    uint32_t ifx, *res;
+    uint8_t *ver;
+    for (uint32_t i = p.lo; i < p.hi; i++) {
+        if (!source_fields(rings, bursts, i, n, ifx, res, ver)) {
+            p.bad = true;
+            return;
         }
+        p.sum += n;
+    }
+}
+
+void part_cut(CutPart &p, const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint64_t ce, uint64_t *start) {
+    p.pieces.clear(), p.first_if.clear(), p.rc.clear(), p.vc.clear();
+    uint64_t pos = p.base, n;
+    uint32_t ifx, *res;
+    uint8_t *ver;
+    for (uint32_t i = p.lo; i < p.hi; i++) {
+        (void)source_fields(rings, bursts, i, n, ifx, res, ver);
         start[i] = pos;
         for (uint64_t a = 0; a < n;) {  // the chunks this source's frames fall in (one, for a small burst)
-            if (chunks.empty() || chunks.back().n == ce) {
-                if (!chunks.empty() && chunks.back().staged) {  // (a staged chunk keeps no copies)
-                    rcopies.resize(chunks.back().r0), vcopies.resize(chunks.back().v0);
-                    chunks.back().r1 = chunks.back().r0, chunks.back().v1 = chunks.back().v0;
-                }
-                const uint32_t r = (uint32_t)rcopies.size(), v = (uint32_t)vcopies.size();
-                chunks.push_back({pos + a, 0, i, i + 1, false, false, false, false, r, r, v, v, {}});
-                first_if = ifx;
+            const uint64_t k = (pos + a) / ce, in = pos + a - k * ce;  // chunk, position in it
+            if (p.pieces.empty() || p.pieces.back().begin != k * ce) {
+                if (!p.pieces.empty()) seal(p.pieces.back(), p.rc, p.vc);
+                const uint32_t r = (uint32_t)p.rc.size(), v = (uint32_t)p.vc.size();
+                p.pieces.push_back({k * ce, 0, i, i + 1, false, false, false, false, r, r, v, v, {}});
+                p.first_if.push_back(ifx);
             }
-            XdpChunk &c = chunks.back();
-            const uint64_t take = std::min(ce - c.n, n - a);
-            c.mixed |= ifx != first_if;
+            XdpChunk &c = p.pieces.back();
+            const uint64_t take = std::min(ce - in, n - a);
+            c.mixed |= ifx != p.first_if.back();
             c.src1 = i + 1;
-            if (res) {
-                c.any_res = true;
-                add_copy(c, rcopies, c.r0, c.r1, c.n, take, reinterpret_cast<uint8_t *>(res + a), 4, c.v1 - c.v0);
+            c.n += take;
+            c.any_res |= res != nullptr, c.any_ver |= ver != nullptr;
+            if (!c.staged) {
+                if (res) append_copy(p.rc, c.r0, c.r1, {in, take, reinterpret_cast<uint8_t *>(res + a)}, 4);
+                if (ver) append_copy(p.vc, c.v0, c.v1, {in, take, ver + a}, 1);
+                c.staged = (c.r1 - c.r0) + (c.v1 - c.v0) > kXdpMaxCopies;
             }
-            if (ver) {
-                c.any_ver = true;
-                add_copy(c, vcopies, c.v0, c.v1, c.n, take, ver + a, 1, c.r1 - c.r0);
-            }
-            c.n += take, a += take;
+            a += take;
         }
         pos += n;
     }
-    if (!chunks.empty() && chunks.back().staged) {
-        rcopies.resize(chunks.back().r0), vcopies.resize(chunks.back().v0);
-        chunks.back().r1 = chunks.back().r0, chunks.back().v1 = chunks.back().v0;
+    if (!p.pieces.empty()) seal(p.pieces.back(), p.rc, p.vc);
+}
+
+// Runs f(t) for t in [0, T): T - 1 helper threads and the calling thread.
+template <class F>
+void run_parts(int T, F &&f) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
+    f(0);
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t chunk,
+               bool auto_chunk, int threads, CutPlan &plan) {
+    constexpr uint32_t kPerThread = 32768;  // sources per thread below which a helper costs more than it saves
+    const int T = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)std::max(threads, 1), count / kPerThread));
+    // the calling thread's shares (their vectors keep their capacity from call to call); the helpers reach them through
+    // this reference — a thread_local named inside the lambdas would be each helper's own, empty, instance
+    thread_local std::vector<CutPart> tl_parts;
+    std::vector<CutPart> &parts = tl_parts;
+    parts.resize(T);
+    for (int t = 0; t < T; t++) {  // (each share's vectors keep their capacity from call to call)
+        parts[t].base = parts[t].sum = 0, parts[t].bad = false;
+        parts[t].lo = (uint32_t)((uint64_t)count * t / T), parts[t].hi = (uint32_t)((uint64_t)count * (t + 1) / T);
     }
-    start[count] = pos;
+    run_parts(T, [&](int t) { part_count(parts[t], rings, bursts); });
+    uint64_t total = 0;
+    for (CutPart &p : parts) {
+        if (p.bad) return -EINVAL;
+        p.base = total, total += p.sum;
+    }
+    plan.start.resize((size_t)count + 1);
+    plan.start[count] = total;
+    plan.src = HostFedSrc{rings, bursts, plan.start.data(), count};
+    plan.ce = chunk_positions(total, chunk, auto_chunk);
+    run_parts(T, [&](int t) { part_cut(parts[t], rings, bursts, plan.ce, plan.start.data()); });
+    // the pieces in order: a chunk shared by two shares is merged (its copies continued, ifindexes compared)
+    std::vector<XdpChunk> &chunks = plan.chunks;
+    std::vector<XdpCopy> &rc = plan.rcopies, &vc = plan.vcopies;
+    chunks.clear(), rc.clear(), vc.clear();
+    uint32_t g_first_if = 0;
+    for (CutPart &p : parts)
+        for (size_t j = 0; j < p.pieces.size(); j++) {
+            const XdpChunk &c = p.pieces[j];
+            if (chunks.empty() || chunks.back().begin != c.begin) {
+                const uint32_t r = (uint32_t)rc.size(), v = (uint32_t)vc.size();
+                chunks.push_back({c.begin, 0, c.src0, c.src1, c.mixed, c.staged, c.any_res, c.any_ver, r, r, v, v, {}});
+                g_first_if = p.first_if[j];
+            } else {
+                XdpChunk &g = chunks.back();
+                g.mixed |= c.mixed || p.first_if[j] != g_first_if;
+                g.src1 = c.src1;
+                g.staged |= c.staged;
+                g.any_res |= c.any_res, g.any_ver |= c.any_ver;
+            }
+            XdpChunk &g = chunks.back();
+            g.n += c.n;
+            if (!g.staged) {
+                for (uint32_t q = c.r0; q < c.r1; q++) append_copy(rc, g.r0, g.r1, p.rc[q], 4);
+                for (uint32_t q = c.v0; q < c.v1; q++) append_copy(vc, g.v0, g.v1, p.vc[q], 1);
+                g.staged = (g.r1 - g.r0) + (g.v1 - g.v0) > kXdpMaxCopies;
+            }
+            seal(g, rc, vc);
+        }
     return 0;
 }
 

@@ -82,13 +82,28 @@ struct XdpChunk {
     infw_hostpack_out out;
 };
 
-// The sources cut into chunks of at most ce positions (ce a multiple of INFW_V6_GROUP), running on from one source
-// into the next, in one pass over the caller's array: fills start (count + 1 entries), chunks (their `out` left for
-// the caller) and their D2H copies.  -EINVAL for a source with flags set or a null array it needs (nothing is packed
-// then).
-int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t ce,
-               std::vector<uint64_t> &start, std::vector<XdpChunk> &chunks, std::vector<XdpCopy> &rcopies,
-               std::vector<XdpCopy> &vcopies, HostFedSrc &src);
+// A call's cut: source positions, chunks and their D2H copies (src.start points into `start`: not copyable).
+struct CutPlan {
+    std::vector<uint64_t> start;  // count + 1 entries
+    std::vector<XdpChunk> chunks;  // their `out` left for the caller
+    std::vector<XdpCopy> rcopies, vcopies;
+    HostFedSrc src;
+    uint64_t ce = 0;  // positions per chunk (the last may hold fewer)
+    CutPlan() = default;
+    CutPlan(const CutPlan &) = delete;
+    CutPlan &operator=(const CutPlan &) = delete;
+};
+
+// Positions per chunk for a call of `total`: `chunk` (a multiple of INFW_V6_GROUP), or with auto_chunk, for a call of
+// fewer than four chunks, a quarter of the call (at least 32K), so that its packing overlaps its copies.
+uint64_t chunk_positions(uint64_t total, uint64_t chunk, bool auto_chunk);
+
+// The sources cut into chunks of chunk_positions(total) positions running on from one source into the next, with
+// their D2H copies: two passes over the caller's array (validate and count, then cut), each split over up to
+// `threads` threads for a call of many sources, whose pieces of a shared chunk are merged in order — the plan is the
+// same at any thread count.  -EINVAL for a source with flags set or a null array it needs (nothing is packed then).
+int cut_chunks(const infw_xdp_ring *rings, const infw_frame_burst *bursts, uint32_t count, uint64_t chunk,
+               bool auto_chunk, int threads, CutPlan &plan);
 
 constexpr uint64_t kPackUnit = 4096;  // descriptors per claimed unit (~30 us of one core's packing)
 

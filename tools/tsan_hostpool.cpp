@@ -11,6 +11,7 @@
 // each chunk (copy runs, or staging past kXdpMaxCopies), played on the host for bursts whose arrays are slices of one
 // array, bursts with arrays of their own, and rings.
 // Prints "tsan_hostpool OK ..." and exits 0.
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -177,23 +178,69 @@ int main() {
         std::vector<infw_xdp_ring> rg = rings;
         for (size_t r = 0; r < rings.size(); r++) rr[r].resize(rings[r].n + 1), rg[r].results = rr[r].data();
         for (uint64_t C : {512ull, 4096ull, 8192ull + 512}) {
-            std::vector<uint64_t> st;
-            std::vector<infw::XdpChunk> ch;
-            std::vector<infw::XdpCopy> rc, vc;
-            infw::HostFedSrc sv;
-            CHECK(infw::cut_chunks(nullptr, sl.data(), (uint32_t)sl.size(), C, st, ch, rc, vc, sv) == 0);
-            for (auto &c : ch) {
+            infw::CutPlan pl;
+            CHECK(infw::cut_chunks(nullptr, sl.data(), (uint32_t)sl.size(), C, false, 1, pl) == 0);
+            for (auto &c : pl.chunks) {
                 CHECK(!c.staged && c.r1 - c.r0 == 1 && c.v1 - c.v0 == 1);  // slices: one copy of each kind per chunk
-                check_copies(c, rc, vc, sv, (uint32_t)C), plans++;
+                check_copies(c, pl.rcopies, pl.vcopies, pl.src, (uint32_t)C), plans++;
             }
-            CHECK(infw::cut_chunks(nullptr, own.data(), (uint32_t)own.size(), C, st, ch, rc, vc, sv) == 0);
-            for (auto &c : ch) check_copies(c, rc, vc, sv, (uint32_t)C + 1), plans++, staged += c.staged;
-            CHECK(infw::cut_chunks(rg.data(), nullptr, (uint32_t)rg.size(), C, st, ch, rc, vc, sv) == 0);
-            for (auto &c : ch) {
+            CHECK(infw::cut_chunks(nullptr, own.data(), (uint32_t)own.size(), C, false, 1, pl) == 0);
+            for (auto &c : pl.chunks) check_copies(c, pl.rcopies, pl.vcopies, pl.src, (uint32_t)C + 1), plans++, staged += c.staged;
+            CHECK(infw::cut_chunks(rg.data(), nullptr, (uint32_t)rg.size(), C, false, 1, pl) == 0);
+            for (auto &c : pl.chunks) {
                 CHECK(!c.staged);
-                check_copies(c, rc, vc, sv, (uint32_t)C + 2), plans++;
+                check_copies(c, pl.rcopies, pl.vcopies, pl.src, (uint32_t)C + 2), plans++;
             }
         }
+        // a call of 150K bursts: the cut split over 1..8 threads is the same plan, chunk for chunk and copy for copy,
+        // whatever falls on the shares' seams (ports and result arrays changing, arrays of their own and slices mixed)
+        std::vector<infw_frame_burst> many;
+        std::vector<uint32_t> mres(1 << 21);
+        std::vector<uint8_t> mver(1 << 21);
+        std::vector<const uint8_t *> ptrs(64, umem.data());
+        std::vector<uint32_t> lens(64, 100);
+        uint64_t at = 0;
+        for (int i = 0; i < 150000; i++) {
+            const uint64_t n = g() % 9;  // 0..8 frames (empty bursts too)
+            infw_frame_burst b{ptrs.data(), lens.data(), nullptr, n, 30 + (uint32_t)(g() % 3 == 0 ? g() % 2 : 0), 0,
+                               nullptr, nullptr};
+            const uint32_t kind = (uint32_t)(g() % 10);
+            if (kind < 6) b.results = mres.data() + at, b.verdicts = kind < 3 ? mver.data() + at : nullptr;  // slices
+            else if (kind < 8) b.results = mres.data() + at + 1;                                               // a gap
+            at += n + (kind >= 6 && kind < 8);
+            many.push_back(b);
+        }
+        for (uint64_t C : {512ull, 4096ull, 1ull << 19}) {
+            for (bool au : {false, true}) {
+                infw::CutPlan ref;
+                CHECK(infw::cut_chunks(nullptr, many.data(), (uint32_t)many.size(), C, au, 1, ref) == 0);
+                for (auto &c : ref.chunks) check_copies(c, ref.rcopies, ref.vcopies, ref.src, (uint32_t)C + 3), plans++;
+                for (int T : {2, 3, 4, 8}) {
+                    infw::CutPlan pl;
+                    CHECK(infw::cut_chunks(nullptr, many.data(), (uint32_t)many.size(), C, au, T, pl) == 0);
+                    CHECK(pl.ce == ref.ce && pl.start == ref.start && pl.chunks.size() == ref.chunks.size());
+                    for (size_t k = 0; k < pl.chunks.size(); k++) {
+                        const infw::XdpChunk &a = pl.chunks[k], &b = ref.chunks[k];
+                        CHECK(a.begin == b.begin && a.n == b.n && a.src0 == b.src0 && a.src1 == b.src1 &&
+                              a.mixed == b.mixed && a.staged == b.staged && a.any_res == b.any_res &&
+                              a.any_ver == b.any_ver && a.r1 - a.r0 == b.r1 - b.r0 && a.v1 - a.v0 == b.v1 - b.v0);
+                        for (uint32_t q = 0; q < a.r1 - a.r0; q++)
+                            CHECK(pl.rcopies[a.r0 + q].pos == ref.rcopies[b.r0 + q].pos &&
+                                  pl.rcopies[a.r0 + q].n == ref.rcopies[b.r0 + q].n &&
+                                  pl.rcopies[a.r0 + q].dst == ref.rcopies[b.r0 + q].dst);
+                        for (uint32_t q = 0; q < a.v1 - a.v0; q++)
+                            CHECK(pl.vcopies[a.v0 + q].pos == ref.vcopies[b.v0 + q].pos &&
+                                  pl.vcopies[a.v0 + q].n == ref.vcopies[b.v0 + q].n &&
+                                  pl.vcopies[a.v0 + q].dst == ref.vcopies[b.v0 + q].dst);
+                    }
+                    plans += pl.chunks.size();
+                }
+            }
+        }
+        // a bad source anywhere (here in the last share) fails the whole cut
+        many[149990].flags = 1;
+        infw::CutPlan bad;
+        CHECK(infw::cut_chunks(nullptr, many.data(), (uint32_t)many.size(), 4096, false, 4, bad) == -EINVAL);
         CHECK(staged > 0);
     }
     uint64_t jobs = 0, chunks_checked = 0, mixed = 0;
@@ -202,13 +249,12 @@ int main() {
         for (uint64_t C : {512ull, 4096ull, 8192ull + 512}) {
             for (int abort_at : {-1, 3, -2}) {  // -2: the bursts, not aborted
                 // the rings (or bursts) cut as classify_host_fed cuts them: chunks of C running on from one to the next
-                std::vector<uint64_t> start;
-                std::vector<infw::XdpChunk> chunks;
-                std::vector<infw::XdpCopy> rc, vc;
-                infw::HostFedSrc src;
+                infw::CutPlan plan;
                 CHECK(abort_at == -2
-                          ? infw::cut_chunks(nullptr, bursts.data(), (uint32_t)bursts.size(), C, start, chunks, rc, vc, src) == 0
-                          : infw::cut_chunks(rings.data(), nullptr, (uint32_t)rings.size(), C, start, chunks, rc, vc, src) == 0);
+                          ? infw::cut_chunks(nullptr, bursts.data(), (uint32_t)bursts.size(), C, false, 1, plan) == 0
+                          : infw::cut_chunks(rings.data(), nullptr, (uint32_t)rings.size(), C, false, 1, plan) == 0);
+                std::vector<infw::XdpChunk> &chunks = plan.chunks;
+                const infw::HostFedSrc &src = plan.src;
                 std::vector<std::vector<uint8_t>> slots(kSlots, std::vector<uint8_t>(32 * C));
                 for (size_t k = 0; k < chunks.size(); k++) {  // the slot layout of abi.cpp, stride S
                     const uint64_t S = (chunks[k].n + 63) & ~63ull;
@@ -238,11 +284,11 @@ int main() {
                 for (int rep = 0; rep < 20; rep++) {
                     const infw_xdp_ring small[2] = {{umem.data(), rd[1].data(), 1, 11, 0, nullptr, nullptr},
                                                     {umem.data(), rd[2].data(), 63, 12, 0, nullptr, nullptr}};
-                    std::vector<uint64_t> ss;
-                    std::vector<infw::XdpChunk> cc;
-                    std::vector<infw::XdpCopy> rc, vc;
-                    infw::HostFedSrc sm;
-                    CHECK(infw::cut_chunks(small, nullptr, 2, 512, ss, cc, rc, vc, sm) == 0 && cc.size() == 1 && cc[0].mixed);
+                    infw::CutPlan sp;
+                    CHECK(infw::cut_chunks(small, nullptr, 2, 512, false, 1, sp) == 0 && sp.chunks.size() == 1 &&
+                          sp.chunks[0].mixed);
+                    std::vector<infw::XdpChunk> &cc = sp.chunks;
+                    const infw::HostFedSrc &sm = sp.src;
                     uint8_t *b = slots[0].data();
                     cc[0].out = {reinterpret_cast<uint32_t *>(b), b + 16 * 64, reinterpret_cast<uint32_t *>(b + 28 * 64),
                                  reinterpret_cast<uint32_t *>(b + 4 * 64), reinterpret_cast<uint32_t *>(b + 8 * 64),
