@@ -56,8 +56,9 @@ struct infw_frame_burst {
 /* are pipelined through the device exactly as for AF_XDP rings (same chunks, */
 /* same options, same results as infw_classify_frames on the same frames).    */
 /* Synchronous; the whole call reads one table epoch.  Hand many bursts to    */
-/* one call (every port's rx bursts of a poll round): the call passes over    */
-/* the array once and copies none of it; result arrays that continue one      */
+/* one call (every port's rx bursts of a poll round): the call copies none   */
+/* of the array (two passes over it, split over up to 8 threads for a call   */
+/* of many bursts); result arrays that continue one                           */
 /* another (slices of one array) come back in one copy per run, arrays of     */
 /* their own are staged per chunk and scattered by the calling thread.        */
 /* -EINVAL for a burst with flags set or a null frames / linear_len array     */
