@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <system_error>
 
 #if defined(__x86_64__)
 #include <immintrin.h>
@@ -316,11 +317,17 @@ void part_cut(CutPart &p, const infw_xdp_ring *rings, const infw_frame_burst *bu
     if (!p.pieces.empty()) seal(p.pieces.back(), p.rc, p.vc);
 }
 
-// Runs f(t) for t in [0, T): T - 1 helper threads and the calling thread.
+// Runs f(t) for t in [0, T): T - 1 helper threads and the calling thread, which also runs the shares of helpers the
+// system would not start (the result does not depend on which thread ran a share).
 template <class F>
 void run_parts(int T, F &&f) {
     std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
+    int started = 1;
+    try {
+        for (; started < T; started++) th.emplace_back([&f, t = started] { f(t); });
+    } catch (const std::system_error &) {
+    }
+    for (int t = started; t < T; t++) f(t);
     f(0);
     for (auto &x : th) x.join();
 }
