@@ -352,3 +352,31 @@ def test_small_bursts_host_match_oracle(setup, arrays):
             b.results[:] = 0xFFFFFFFF
             b.verdicts[:] = 7
     del buf
+
+
+def test_many_bursts_threaded_cut_match_oracle(setup):
+    """A call of more than 65536 bursts (1..2 frames each, ports interleaved, result arrays slices of one array with a
+    gap now and then): the cut runs in two passes split over several threads (hostfeed.cpp cut_chunks), and the call
+    still gives the oracle's words, verdicts and counters."""
+    from test_hostpack_cpu import _burst_of
+    wl, clf, m = setup
+    n = 110000
+    hdr, cap, pl, ifx = wl.frames(2000000, n)
+    buf, whole, _ = _burst_of(hdr, cap, pl, 0, stride=128)
+    want_r, want_v, wst, _ = m.classify_frames(hdr, cap, pl, ifx, nthreads=8)
+    rng = np.random.default_rng(77)
+    res = np.full(n + n // 8, 0xFFFFFFFF, np.uint32)
+    bursts, at, gap = [], 0, 0
+    while at < n:
+        hi = at + 1 if rng.random() < 0.5 or at + 1 == n or ifx[at + 1] != ifx[at] else at + 2
+        gap += rng.random() < 0.05  # a burst whose words do not continue the previous one's
+        bursts.append((at, hi, gap, infw.Burst(whole.frames[at:hi], cap[at:hi], pl[at:hi], int(ifx[at]),
+                                               results=res[at + gap:hi + gap])))
+        at = hi
+    assert len(bursts) > 65536
+    clf.stats_reset()
+    clf.classify_bursts_host(infw.BurstArray([b for _, _, _, b in bursts]))
+    for lo, hi, _, b in bursts:
+        assert np.array_equal(b.results, want_r[lo:hi]), lo
+    assert np.array_equal(clf.stats_read_all(), wst)
+    del buf
