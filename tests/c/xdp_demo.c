@@ -7,6 +7,9 @@
  * 8 are two calls.  Then the same frames through the host-fed path, infw_classify_xdp_host, with the memory as the
  * daemon allocated it (pageable, unregistered — the form a socket's mmapped ring has): both rings in one call.  Before
  * any registration, infw_classify_xdp must refuse that memory with -EFAULT rather than let the GPU fault on it.
+ * Last, the same packets as a DPDK poll loop hands them over (infw_classify_bursts_host): every frame in a buffer of
+ * its own (an mbuf's data room), one pointer, data_len and pkt_len per frame — one frame split over two segments —
+ * one burst per port, the bursts' result words slices of one array; and the burst's deny events.
  *
  *   the XDP entry per frame (kernel.c:459-462, ethertype / L4 extraction :95-174, :412-440)
  *   statsMap.Lookup (statistics.go:127):  infw_stats_read
@@ -133,9 +136,27 @@ int main(int argc, char **argv) {
             fprintf(stderr, "host events: %llu events, size %u\n", (unsigned long long)n_ev, ev[0].size);
             return 1;
         }
+        const uint8_t *fp[N];
+        uint32_t fl[N];
+        for (int i = 0; i < N; i++) fp[i] = umem + rx[i].addr, fl[i] = rx[i].len;
+        const struct infw_frame_burst hb = {fp, fl, NULL, N - 1, 7, 0, results, NULL};
+        rc = infw_classify_bursts_host(ctx, 0, &hb, 1, 0);
+        if (rc != -ENODEV) {
+            fprintf(stderr, "host-only classify_bursts_host returned %d, want -ENODEV\n", rc);
+            return 1;
+        }
+        uint32_t s4b[N], plb[N], mb[N], l4b[N];
+        uint8_t tailb[768];
+        const struct infw_batch_soa_c_out ob = {s4b, tailb, NULL, plb, mb, l4b};
+        CHECK(infw_pack_burst_host(&hb, &ob));
+        for (int i = 0; i < N - 1; i++)
+            if (s4b[i] != s4[i] || plb[i] != plen[i] || mb[i] != meta[i] || l4b[i] != l4[i]) {
+                fprintf(stderr, "pack_burst_host: frame %d differs from pack_xdp_host\n", i);
+                return 1;
+            }
         infw_destroy(ctx);
-        printf("xdp_demo OK (host): classify_xdp and classify_xdp_host refused without a device, the host packer "
-               "alone packed %d frames, ABI %d\n", N, infw_abi_version());
+        printf("xdp_demo OK (host): classify_xdp, classify_xdp_host and classify_bursts_host refused without a device, "
+               "the host packers alone packed %d frames (rings and bursts alike), ABI %d\n", N, infw_abi_version());
         return 0;
     }
     {
@@ -224,10 +245,47 @@ int main(int argc, char **argv) {
         fprintf(stderr, "host events: %llu events, size %u\n", (unsigned long long)n_ev, ev[0].size);
         return 1;
     }
+
+    /* DPDK-style: each frame in a buffer of its own (an mbuf's data room, at a 128-B headroom); packet 1's frame split
+     * over two segments after 60 B (data_len 60 < pkt_len 200: kernel.c reads only the linear part, and its bytes are
+     * all inside it); one burst per port; result words as slices of one array, verdicts not wanted */
+    uint8_t *mbuf[N];
+    const uint8_t *ptr[N];
+    uint32_t dlen[N], plen2[N], res[N];
+    for (int i = 0; i < N; i++) {
+        if (posix_memalign((void **)&mbuf[i], 64, 2048)) return 1;
+        memset(mbuf[i], 0, 2048);
+        memcpy(mbuf[i] + 128, umem + rx[i].addr, pk[i].len);
+        ptr[i] = mbuf[i] + 128, plen2[i] = pk[i].len, dlen[i] = i == 1 ? 60 : pk[i].len;
+    }
+    memset(res, 0xFF, sizeof(res));
+    const struct infw_frame_burst bursts[2] = {{ptr, dlen, plen2, N - 1, 7, 0, res, NULL},
+                                               {ptr + N - 1, dlen + N - 1, plen2 + N - 1, 1, 8, 0, res + N - 1, NULL}};
+    CHECK(infw_classify_bursts_host(ctx, 0, bursts, 2, 0));
+    for (int i = 0; i < N; i++)
+        if (res[i] != want_r[i]) {
+            fprintf(stderr, "burst frame %d: result 0x%x, want 0x%x\n", i, res[i], want_r[i]);
+            return 1;
+        }
+    CHECK(infw_stats_read_all(ctx, all));
+    uint64_t allow3 = 0, deny3 = 0;
+    for (int rule = 1; rule < 100; rule++) allow3 += all[rule].allow_stats.packets, deny3 += all[rule].deny_stats.packets;
+    if (allow3 != 3 * allow || deny3 != 3 * deny) {
+        fprintf(stderr, "burst counters: allow %llu deny %llu\n", (unsigned long long)allow3, (unsigned long long)deny3);
+        return 1;
+    }
+    n_ev = 0;
+    CHECK(infw_burst_host_events(&bursts[0], res, ev, 2, &n_ev));
+    if (n_ev != 1 || ev[0].size != ((8 + 100 + 4 + 7) & ~7) - 4 || memcmp(ev[0].raw + 8, ptr[0], 100) != 0) {
+        fprintf(stderr, "burst events: %llu events, size %u\n", (unsigned long long)n_ev, ev[0].size);
+        return 1;
+    }
+    for (int i = 0; i < N; i++) free(mbuf[i]);
     infw_destroy(ctx);
     free(umem), free(rx), free(results), free(verdicts);
     printf("xdp_demo OK: %d frames in 2 rings, allow %llu (%llu B), deny %llu (%llu B); pageable memory refused by the "
-           "device read (-EFAULT) and classified by the host-fed path, its deny event built on the host, ABI %d\n", N,
+           "device read (-EFAULT) and classified by the host-fed path, its deny event built on the host; the same "
+           "frames as DPDK-style bursts (one split over two segments) give the same words and event, ABI %d\n", N,
            (unsigned long long)allow, (unsigned long long)allow_b, (unsigned long long)deny,
            (unsigned long long)deny_b, infw_abi_version());
     return 0;
