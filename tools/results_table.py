@@ -7,7 +7,7 @@ run's launches); roofline.frac (algorithmic bytes / HIP-event time / 8 TB/s); HB
 requests (TCC_EA0_RDREQ) x 128 B per second against the stream bandwidth the same line measured in its own process,
 and its inverse (the most the kernel could gain at today's lines per packet if every random line moved at the
 streaming rate).  Lines whose build id differs from the profile's are refused.
-Usage: tools/results_table.py <pass> [<override pass>]  (e.g. r06z r06G: lines present in profiles/<override>/lines,
+Usage: tools/results_table.py <pass> [<override pass>]  (e.g. r06z r06K: lines present in profiles/<override>/lines,
 and profiles <override>_<key>, replace the pass's own — re-measured after a host-side change at the same kernel build)
   -> markdown on stdout, JSON in profiles/<override or pass>/results.json"""
 import json
