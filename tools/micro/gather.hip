@@ -40,6 +40,57 @@ __global__ __launch_bounds__(512, 8) void gather(const uint32_t *__restrict__ ta
     out[tid] = acc;
 }
 
+// Scalar-path gathers (the "mix" test): of every wave's 64 lookups, the first kScalar lanes' go through the scalar
+// data cache one at a time — readlane makes the index wave-uniform, so the 8-B load is an s_load — and the other lanes'
+// are ordinary per-lane vector loads.  Does the scalar path add random-gather capacity beside the vector L1's?
+template <int kScalar>
+__global__ __launch_bounds__(512, 8) void gather_mix(const uint2 *__restrict__ tab, uint32_t mask, int iters,
+                                                     uint32_t *__restrict__ out) {
+    const uint32_t tid = blockIdx.x * 512 + threadIdx.x, lane = threadIdx.x & 63;
+    uint32_t acc = 0, idx = mix(tid);
+    for (int it = 0; it < iters; it++) {
+        const uint32_t rec = mix(idx + it * 0x9E3779B9u) & mask;
+        uint2 vv = make_uint2(0, 0);
+        if (lane >= (uint32_t)kScalar) vv = tab[rec];  // the vector lanes' loads first, consumed last
+        // all the wave's scalar loads issued before any is consumed (up to 16 in flight per wave: SGPR budget)
+        uint2 sv = make_uint2(0, 0);
+#pragma unroll
+        for (int j0 = 0; j0 < kScalar; j0 += 16) {
+            uint2 v[16];
+#pragma unroll
+            for (int j = 0; j < 16 && j0 + j < kScalar; j++) v[j] = tab[__builtin_amdgcn_readlane(rec, j0 + j)];
+#pragma unroll
+            for (int j = 0; j < 16 && j0 + j < kScalar; j++)
+                if (lane == (uint32_t)(j0 + j)) sv = v[j];
+        }
+        acc += lane >= (uint32_t)kScalar ? (vv.x ^ vv.y) : (sv.x ^ sv.y);
+    }
+    out[tid] = acc;
+}
+
+template <int kScalar>
+void run_mix(const uint32_t *tab, uint64_t tbytes, uint32_t *out, int grid, int iters) {
+    const uint32_t mask = (uint32_t)(tbytes / 8 - 1);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    gather_mix<kScalar><<<grid, 512>>>(reinterpret_cast<const uint2 *>(tab), mask, iters, out);
+    hipEventRecord(a);
+    const int reps = 5;
+    for (int r = 0; r < reps; r++)
+        gather_mix<kScalar><<<grid, 512>>>(reinterpret_cast<const uint2 *>(tab), mask, iters, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double lookups = (double)grid * 512 * iters * reps;
+    printf("{\"test\": \"mix\", \"scalar_lanes\": %d, \"table_MiB\": %.1f, \"Glookups_s\": %.2f, "
+           "\"scalar_Glookups_s\": %.2f, \"vector_Glookups_s\": %.2f}\n",
+           kScalar, tbytes / 1048576.0, lookups / (ms * 1e-3) / 1e9, lookups * kScalar / 64 / (ms * 1e-3) / 1e9,
+           lookups * (64 - kScalar) / 64 / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+}
+
 // Spread footprint: `lines` distinct 128-B lines (16 B read from each), one at a random 128-B slot of each
 // `stride`-byte window, so the L2 footprint stays the same while the address span (pages the lookups
 // touch) grows with the stride.
@@ -112,6 +163,17 @@ int main(int argc, char **argv) {
         for (uint64_t f : {64ull << 20, 1ull << 30})
             for (uint64_t span : {1ull << 30, 2ull << 30, 4ull << 30, 8ull << 30, 12ull << 30})
                 run_spread(tab, f, span, out, grid, 64);
+        return 0;
+    }
+    if (argc > 1 && strcmp(argv[1], "mix") == 0) {  // scalar-path gathers beside vector ones
+        for (uint64_t t : {1ull << 20, 16ull << 20, 1ull << 30}) {
+            run_mix<0>(tab, t, out, grid, 16);
+            run_mix<4>(tab, t, out, grid, 16);
+            run_mix<8>(tab, t, out, grid, 16);
+            run_mix<16>(tab, t, out, grid, 16);
+            run_mix<32>(tab, t, out, grid, 16);
+            run_mix<64>(tab, t, out, grid, 16);
+        }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 's') {  // "spread": same L2 footprint over a growing address span
