@@ -1,7 +1,8 @@
 #!/bin/bash
-# configs[2] under per-context options (results identical; tools-only sweep), alternated twice
+# configs[2] under each per-context table option (results identical; the counters' digest is printed), alternated
+# twice on one box.  Usage (GPU box): tools/opt_sweep.sh [out_dir]   (default gpurun_out/opts)
 set -u
-O=gpurun_out/r06K_opts; mkdir -p $O
+O=${1:-gpurun_out/opts}; mkdir -p $O
 for r in 1 2; do
   for o in "" "--opt dt_parts=8" "--opt dt_parts=4" "--opt dt_half=1" "--opt dt_half=0" "--opt d16=1" "--opt dt_adapt=0"; do
     tag=$(echo "base $o" | tr ' =' '__')
